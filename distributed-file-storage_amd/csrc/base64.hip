@@ -1,0 +1,296 @@
+// base64.hip — RFC 4648 Base64 encode / decode for gfx950 (MI355X).
+//
+// Encode replaces Base64.getEncoder().encodeToString(f.data) inside
+// buildFragmentsJson (StorageNode.java:636); decode replaces
+// Base64.getDecoder().decode(fragInfo.get("data")) in
+// handleInternalStoreFragments (StorageNode.java:281), including the JDK
+// basic decoder's IllegalArgumentException cases.
+//
+// Both kernels are HBM-bound byte streams: 12 input bytes
+// -> 16 chars per lane-step, 64 lanes of a wave touch 768 contiguous input
+// bytes and 1 KiB of contiguous output, the 6-bit -> ASCII map (and its
+// inverse) is a table in LDS, and misaligned starts are fixed in registers
+// with v_alignbyte / v_perm so every global access is dword aligned.
+#include "stream_common.h"
+
+namespace dfs {
+namespace {
+
+__constant__ uint32_t kAlphaWords[16] = {
+    // "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/" as LE words
+    0x44434241u, 0x48474645u, 0x4c4b4a49u, 0x504f4e4du, 0x54535251u, 0x58575655u, 0x62615a59u, 0x66656463u,
+    0x6a696867u, 0x6e6d6c6bu, 0x7271706fu, 0x76757473u, 0x7a797877u, 0x33323130u, 0x37363534u, 0x2f2b3938u};
+
+__device__ __forceinline__ uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+
+// Four ASCII chars (first char in the low byte) of one 24-bit group.
+__device__ __forceinline__ uint32_t enc4(const uint8_t* __restrict__ lut, uint32_t v) {
+    const uint32_t c0 = lut[v >> 18];
+    const uint32_t c1 = lut[(v >> 12) & 63u];
+    const uint32_t c2 = lut[(v >> 6) & 63u];
+    const uint32_t c3 = lut[v & 63u];
+    return c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+}
+
+__global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t* __restrict__ base,
+                                                                  const StreamJob* __restrict__ jobs,
+                                                                  uint32_t njobs, uint64_t ntiles,
+                                                                  char* __restrict__ out) {
+    __shared__ uint32_t lut_words[16];
+    if (threadIdx.x < 16) lut_words[threadIdx.x] = kAlphaWords[threadIdx.x];
+    __syncthreads();
+    const uint8_t* lut = reinterpret_cast<const uint8_t*>(lut_words);
+
+    uint64_t t0, t1;
+    tile_range(ntiles, t0, t1);
+    if (t0 >= t1) return;
+    uint32_t j = find_job(jobs, njobs, t0);
+    for (uint64_t t = t0; t < t1; ++t) {
+        while (jobs[j + 1].tile_start <= t) ++j;
+        const uint64_t len = jobs[j].len;
+        const uint64_t nfg = len / 12;  // full 12-byte groups
+        const uint32_t rem = static_cast<uint32_t>(len - 12 * nfg);
+        const uint8_t* __restrict__ src = base + jobs[j].src_off;
+        uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(out) + jobs[j].dst_off;
+        const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
+        const uint64_t g0 = (t - jobs[j].tile_start) * kEncGroupsPerTile + threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < kEncGroupsPerTile / kStreamBlock; ++i) {
+            const uint64_t g = g0 + static_cast<uint64_t>(i) * kStreamBlock;
+            if (g < nfg) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + 12 * g - sa);
+                uint32_t u0, u1, u2;
+                if (sa) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(w);
+                    u0 = align_bytes(v.y, v.x, sa);
+                    u1 = align_bytes(v.z, v.y, sa);
+                    u2 = align_bytes(v.w, v.z, sa);
+                } else {
+                    u0 = w[0]; u1 = w[1]; u2 = w[2];
+                }
+                // Big-endian 24-bit groups: bytes (0,1,2) (3,4,5) (6,7,8) (9,10,11).
+                const uint32_t g0v = __builtin_amdgcn_perm(0u, u0, 0x0c000102u);
+                const uint32_t g1v = __builtin_amdgcn_perm(u1, u0, 0x0c030405u);
+                const uint32_t g2v = __builtin_amdgcn_perm(u2, u1, 0x0c020304u);
+                const uint32_t g3v = __builtin_amdgcn_perm(0u, u2, 0x0c010203u);
+                const uint4 o = make_uint4(enc4(lut, g0v), enc4(lut, g1v), enc4(lut, g2v), enc4(lut, g3v));
+                *reinterpret_cast<uint4*>(dst + 16 * g) = o;
+            } else if (g == nfg && rem) {
+                // Last partial group: full triples then "==" / "=" padding (RFC 4648 §4).
+                uint32_t* o = reinterpret_cast<uint32_t*>(dst + 16 * g);
+                const uint8_t* s = src + 12 * g;
+                for (uint32_t k = 0; k < rem; k += 3) {
+                    const uint32_t n = rem - k < 3 ? rem - k : 3;
+                    uint32_t v = static_cast<uint32_t>(s[k]) << 16;
+                    if (n > 1) v |= static_cast<uint32_t>(s[k + 1]) << 8;
+                    if (n > 2) v |= s[k + 2];
+                    uint32_t wv = enc4(lut, v);
+                    if (n == 1) wv = (wv & 0x0000ffffu) | 0x3d3d0000u;  // "xx=="
+                    else if (n == 2) wv = (wv & 0x00ffffffu) | 0x3d000000u;  // "xxx="
+                    o[k / 3] = wv;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Decode.
+// Message of L chars: q = L/4 full units, r = L%4.
+//   r == 1           -> IllegalArgumentException (dangling char / bad ending)
+//   r == 2, 3        -> q body units + a final unit of r alphabet chars
+//   r == 0, q >= 1   -> q-1 body units + a final unit "xxxx" | "xxx=" | "xx=="
+// Body units must be 4 alphabet chars.  Output byte i goes to dst + i.
+// With h = bytes up to the first 4-aligned output address, item c < nc writes
+// output bytes [h+12c, h+12c+12) as three aligned dwords; item nc (the "tail"
+// item) writes the head and tail bytes, decodes the final unit, validates
+// the body units no main item owns and sets status / out_len.
+// ---------------------------------------------------------------------------
+struct DecGeom {
+    uint64_t body_units;
+    uint64_t nb;   // body bytes
+    uint32_t h;    // head bytes
+    uint64_t nc;   // main items
+    uint32_t u_first;  // first unit owned by main items (h == 3)
+};
+
+__device__ __forceinline__ DecGeom dec_geom(uint64_t L, uintptr_t dst) {
+    DecGeom g;
+    const uint64_t q = L >> 2;
+    const uint32_t r = static_cast<uint32_t>(L & 3u);
+    g.body_units = (r == 0) ? (q ? q - 1 : 0) : q;
+    g.nb = 3 * g.body_units;
+    g.h = static_cast<uint32_t>((4u - (dst & 3u)) & 3u);
+    g.nc = g.nb > g.h ? (g.nb - g.h) / 12 : 0;
+    g.u_first = g.h == 3 ? 1u : 0u;
+    return g;
+}
+
+// 6-bit value of each char; 0xFF for anything outside the alphabet ('=' too).
+__device__ __forceinline__ void build_dec_lut(uint8_t* lut) {
+    for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) {
+        uint32_t v = 0xFFu;
+        if (c >= 'A' && c <= 'Z') v = c - 'A';
+        else if (c >= 'a' && c <= 'z') v = c - 'a' + 26;
+        else if (c >= '0' && c <= '9') v = c - '0' + 52;
+        else if (c == '+') v = 62;
+        else if (c == '/') v = 63;
+        lut[c] = static_cast<uint8_t>(v);
+    }
+}
+
+// Decode the 4 chars (LE word) of one unit: returns 24-bit value, ORs the raw
+// lookups into `bad` (bit 7+ set iff a char is outside the alphabet).
+__device__ __forceinline__ uint32_t dec_unit(const uint8_t* __restrict__ lut, uint32_t w, uint32_t& bad) {
+    const uint32_t d0 = lut[w & 255u], d1 = lut[(w >> 8) & 255u], d2 = lut[(w >> 16) & 255u], d3 = lut[w >> 24];
+    bad |= d0 | d1 | d2 | d3;
+    return (d0 << 18) | (d1 << 12) | (d2 << 6) | d3;
+}
+
+// Value of char at index i of a message (tail path, byte loads).
+__device__ __forceinline__ uint32_t dec_char(const uint8_t* __restrict__ lut, const uint8_t* s, uint64_t i) {
+    return lut[s[i]];
+}
+
+__device__ __forceinline__ uint32_t dec_unit_bytes(const uint8_t* __restrict__ lut, const uint8_t* s, uint64_t u,
+                                                   uint32_t& bad) {
+    const uint32_t d0 = lut[s[4 * u]], d1 = lut[s[4 * u + 1]], d2 = lut[s[4 * u + 2]], d3 = lut[s[4 * u + 3]];
+    bad |= d0 | d1 | d2 | d3;
+    return (d0 << 18) | (d1 << 12) | (d2 << 6) | d3;
+}
+
+__global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
+                                                                  const StreamJob* __restrict__ jobs,
+                                                                  uint32_t njobs, uint64_t ntiles,
+                                                                  uint8_t* __restrict__ out,
+                                                                  int32_t* __restrict__ status,
+                                                                  uint64_t* __restrict__ out_len) {
+    __shared__ uint8_t lut[256];
+    build_dec_lut(lut);
+    __syncthreads();
+
+    uint64_t t0, t1;
+    tile_range(ntiles, t0, t1);
+    if (t0 >= t1) return;
+    uint32_t j = find_job(jobs, njobs, t0);
+    for (uint64_t t = t0; t < t1; ++t) {
+        while (jobs[j + 1].tile_start <= t) ++j;
+        const uint64_t L = jobs[j].len;
+        const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(in) + jobs[j].src_off;
+        uint8_t* __restrict__ dst = out + jobs[j].dst_off;
+        const DecGeom G = dec_geom(L, reinterpret_cast<uintptr_t>(dst));
+        const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
+        const uint32_t id = jobs[j].id;
+        const uint64_t c0 = (t - jobs[j].tile_start) * kDecChunksPerTile + threadIdx.x;
+        const uint32_t e = G.h % 3u;                  // byte offset inside the first unit used
+        const bool five = (G.h == 1u || G.h == 2u);   // chunk straddles 5 units
+#pragma unroll
+        for (int i = 0; i < kDecChunksPerTile / kStreamBlock; ++i) {
+            const uint64_t c = c0 + static_cast<uint64_t>(i) * kStreamBlock;
+            if (c < G.nc) {
+                const uint64_t U = 4 * c + G.u_first;  // first unit read
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + 4 * U - sa);
+                uint32_t raw[6];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) raw[k] = w[k];
+                raw[4] = (sa || five) ? w[4] : 0u;
+                raw[5] = (sa && five) ? w[5] : 0u;
+                uint32_t cw[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) cw[k] = align_bytes(raw[k + 1], raw[k], sa);
+                uint32_t bad = 0, bad5 = 0;
+                const uint32_t v0 = dec_unit(lut, cw[0], bad);
+                const uint32_t v1 = dec_unit(lut, cw[1], bad);
+                const uint32_t v2 = dec_unit(lut, cw[2], bad);
+                const uint32_t v3 = dec_unit(lut, cw[3], bad);
+                const uint32_t v4 = five ? dec_unit(lut, cw[4], bad5) : 0u;
+                if (bad & 0x80u) atomicOr(status + id, 1);
+                // 15 decoded bytes as LE words, then shift by e bytes.
+                const uint32_t x0 = __builtin_amdgcn_perm(v1, v0, 0x06000102u);
+                const uint32_t x1 = __builtin_amdgcn_perm(v2, v1, 0x05060001u);
+                const uint32_t x2 = __builtin_amdgcn_perm(v3, v2, 0x04050600u);
+                const uint32_t x3 = __builtin_amdgcn_perm(0u, v4, 0x0c000102u);
+                uint32_t* o = reinterpret_cast<uint32_t*>(dst + G.h + 12 * c);
+                o[0] = align_bytes(x1, x0, e);
+                o[1] = align_bytes(x2, x1, e);
+                o[2] = align_bytes(x3, x2, e);
+            } else if (c == G.nc) {
+                // ---- tail item ----
+                uint32_t bad = 0;
+                const uint32_t r = static_cast<uint32_t>(L & 3u);
+                bool err = (r == 1u);
+                // Body units no main item validated.
+                const uint64_t covered_end = G.u_first + 4 * G.nc;
+                for (uint64_t u = 0; u < G.body_units; ++u) {
+                    if (u >= G.u_first && u < covered_end) { u = covered_end - 1; continue; }
+                    dec_unit_bytes(lut, src, u, bad);
+                }
+                // Final unit.
+                uint32_t fin_bytes = 0, fin_val = 0;
+                if (!err && L) {
+                    const uint64_t f = 4 * G.body_units;  // first char of the final unit
+                    if (r == 0) {
+                        const uint32_t c2 = src[f + 2], c3 = src[f + 3];
+                        const uint32_t d0 = dec_char(lut, src, f), d1 = dec_char(lut, src, f + 1);
+                        const uint32_t d2 = lut[c2], d3 = lut[c3];
+                        if ((d0 | d1) & 0x80u) err = true;
+                        else if (c2 == '=' && c3 == '=') { fin_bytes = 1; fin_val = (d0 << 18) | (d1 << 12); }
+                        else if (!(d2 & 0x80u) && c3 == '=') { fin_bytes = 2; fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6); }
+                        else if (!((d2 | d3) & 0x80u)) { fin_bytes = 3; fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6) | d3; }
+                        else err = true;
+                    } else {  // r == 2 or 3: unpadded final unit
+                        const uint32_t d0 = dec_char(lut, src, f), d1 = dec_char(lut, src, f + 1);
+                        const uint32_t d2 = r == 3 ? dec_char(lut, src, f + 2) : 0u;
+                        if ((d0 | d1 | d2) & 0x80u) err = true;
+                        fin_bytes = r - 1;
+                        fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6);
+                    }
+                }
+                if (bad & 0x80u) err = true;
+                const uint64_t total = err ? 0 : G.nb + fin_bytes;
+                if (!err) {
+                    // Head bytes [0, min(h, nb)) and tail bytes [h + 12nc, total).
+                    auto byte_at = [&](uint64_t i) -> uint8_t {
+                        const uint64_t u = i / 3;
+                        uint32_t b2 = 0;
+                        const uint32_t v = (u < G.body_units) ? dec_unit_bytes(lut, src, u, b2) : fin_val;
+                        return static_cast<uint8_t>(v >> (16 - 8 * static_cast<uint32_t>(i % 3)));
+                    };
+                    const uint64_t head_end = G.h < total ? G.h : total;
+                    for (uint64_t i = 0; i < head_end; ++i) dst[i] = byte_at(i);
+                    for (uint64_t i = G.h + 12 * G.nc; i < total; ++i) {
+                        if (i < head_end) continue;
+                        dst[i] = byte_at(i);
+                    }
+                }
+                const uint64_t expect = jobs[j].expect;
+                int32_t flags = err ? 1 : 0;
+                if (expect && !err && total + 1 != expect) flags |= 2;
+                if (flags) atomicOr(status + id, flags);
+                if (out_len) out_len[id] = total;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, char* out,
+                             hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(b64_encode_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, base, jobs, njobs,
+                       ntiles, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
+                             int32_t* status, uint64_t* out_len, hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(b64_decode_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, in, jobs, njobs,
+                       ntiles, out, status, out_len);
+    return hipGetLastError();
+}
+
+}  // namespace dfs

@@ -1,0 +1,860 @@
+// dfs_gpu.cpp — C ABI of libdfsgpu.so (include/dfs_gpu.h).
+//
+// Owns the HIP context state (streams, events, device scratch), builds the
+// per-batch descriptor tables on the host (split plan, Base64 offsets,
+// length-sorted SHA lanes) and launches the gfx950 kernels.  There is no CPU
+// implementation of any data-path step here: without a gfx950 device
+// dfs_open fails and nothing runs.
+//
+// Reference sites replaced (StorageNode.java, SN:line): sha256Hex :603-613
+// (called at :127, :159, :282, :454); split loop :138-171; Base64 encode
+// :636; Base64 decode :281; ordered gather :422-451; verify :454-458.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/dfs_gpu.h"
+#include "dfs_internal.h"
+
+using dfs::ShaDesc;
+using dfs::StreamJob;
+
+namespace {
+
+constexpr uint64_t kMaxMsg = 1ull << 37;  // nfull (len/64) must fit 32 bits
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = n < 256 ? 256 : n;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_EXPECT, B_COUNT };
+
+}  // namespace
+
+struct dfs_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;   // default stream of this ctx
+    hipStream_t aux = nullptr;   // second stream (Base64 beside SHA)
+    hipStream_t user = nullptr;  // borrowed (dfs_set_stream)
+    bool profiling = false;
+    hipEvent_t ev[2 * DFS_T_COUNT] = {};
+    bool ev_used[DFS_T_COUNT] = {};
+    DevBuf buf[B_COUNT];
+    std::mutex mu;
+    hipStream_t stream() const { return user ? user : own; }
+};
+
+struct dfs_upload_plan {
+    int device = 0;
+    uint32_t nfiles = 0, nfrag = 0;
+    uint32_t n_all = 0, n_frag_only = 0;  // SHA lanes with / without fileIds
+    uint32_t prio_all = 0, prio_frag = 0;
+    ShaDesc* d_all = nullptr;
+    ShaDesc* d_frag = nullptr;
+    StreamJob* d_enc = nullptr;
+    uint32_t n_enc = 0;
+    uint64_t enc_tiles = 0;
+    std::vector<uint64_t> b64_off;
+    uint64_t b64_total = 0;
+};
+
+namespace {
+
+thread_local char g_last_hip[160];
+
+int hip_fail(hipError_t e, const char* what) {
+    std::snprintf(g_last_hip, sizeof g_last_hip, "%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? DFS_E_NOMEM : DFS_E_HIP;
+}
+
+#define HIPC(x)                                   \
+    do {                                          \
+        hipError_t e_ = (x);                      \
+        if (e_ != hipSuccess) return hip_fail(e_, #x); \
+    } while (0)
+
+void split(uint64_t S, uint32_t N, uint64_t* off, uint64_t* len) {
+    const uint64_t base = S / N, rem = S % N;  // SN:140-141
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+        const uint64_t part = base + (i < rem ? 1 : 0);  // SN:155
+        off[i] = o;
+        len[i] = part;
+        o += part;  // SN:170
+    }
+}
+
+uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
+
+// Sort SHA lanes longest-first (uniform waves) and count the lanes that
+// carry the long chains: those waves get issue priority in the kernel.
+uint32_t sort_lanes(std::vector<ShaDesc>& d) {
+    std::stable_sort(d.begin(), d.end(), [](const ShaDesc& a, const ShaDesc& b) { return a.len > b.len; });
+    if (d.size() < 2) return 0;
+    const uint64_t med = d[d.size() / 2].len;
+    uint32_t n = 0;
+    while (n < d.size() && d[n].len >= 2 * med + 64) ++n;
+    return (n + 63) & ~63u;
+}
+
+// Fill tile_start prefix for `items` work items per job; append sentinel.
+uint64_t finish_jobs(std::vector<StreamJob>& jobs, const std::vector<uint64_t>& items, uint64_t per_tile) {
+    uint64_t t = 0;
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        jobs[i].tile_start = t;
+        t += (items[i] + per_tile - 1) / per_tile;
+    }
+    StreamJob s{};
+    s.tile_start = t;
+    jobs.push_back(s);
+    return t;
+}
+
+// Decode geometry (must match dec_geom in base64.hip): items = nc + 1.
+uint64_t dec_items(uint64_t L, uintptr_t dst) {
+    const uint64_t q = L >> 2;
+    const uint32_t r = static_cast<uint32_t>(L & 3u);
+    const uint64_t body_units = (r == 0) ? (q ? q - 1 : 0) : q;
+    const uint64_t nb = 3 * body_units;
+    const uint32_t h = static_cast<uint32_t>((4u - (dst & 3u)) & 3u);
+    const uint64_t nc = nb > h ? (nb - h) / 12 : 0;
+    return nc + 1;
+}
+
+uint64_t copy_items(uint64_t len, uintptr_t dst) {
+    if (!len) return 0;
+    const uint32_t h = static_cast<uint32_t>((4u - (dst & 3u)) & 3u);
+    const uint64_t nc = len > h ? (len - h) / 16 : 0;
+    return nc + 1;
+}
+
+struct Timer {
+    dfs_ctx* c;
+    explicit Timer(dfs_ctx* ctx) : c(ctx) {
+        for (bool& u : c->ev_used) u = false;
+    }
+    void begin(int k, hipStream_t s) {
+        if (!c->profiling) return;
+        (void)hipEventRecord(c->ev[2 * k], s);
+    }
+    void end(int k, hipStream_t s) {
+        if (!c->profiling) return;
+        (void)hipEventRecord(c->ev[2 * k + 1], s);
+        c->ev_used[k] = true;
+    }
+};
+
+int put(dfs_ctx* c, int id, const void* src, size_t n, hipStream_t s) {
+    HIPC(c->buf[id].ensure(n));
+    if (n) HIPC(hipMemcpyAsync(c->buf[id].p, src, n, hipMemcpyHostToDevice, s));
+    return DFS_OK;
+}
+
+int enter(dfs_ctx* c) {
+    if (!c) return DFS_E_ARG;
+    HIPC(hipSetDevice(c->device));
+    return DFS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfs_abi_version(void) { return DFS_ABI_VERSION; }
+
+const char* dfs_strerror(int code) {
+    switch (code) {
+        case DFS_OK: return "ok";
+        case DFS_E_ARG: return "invalid argument";
+        case DFS_E_HIP: return g_last_hip[0] ? g_last_hip : "HIP runtime error";
+        case DFS_E_NOMEM: return "out of device memory";
+        case DFS_E_DECODE: return "Illegal base64 input (IllegalArgumentException)";
+        case DFS_E_MISSING: return "Could not retrieve fragment";
+        case DFS_E_CORRUPT: return "File corrupted";
+        case DFS_E_FRAG_MISMATCH: return "Hash mismatch on fragment";
+        case DFS_E_NODEV: return "no gfx950 (MI355X) device available";
+        default: return "unknown error";
+    }
+}
+
+int dfs_open(dfs_ctx** out, int device) {
+    if (!out) return DFS_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return DFS_E_NODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return DFS_E_NODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DFS_E_NODEV;
+    dfs_ctx* c = new (std::nothrow) dfs_ctx;
+    if (!c) return DFS_E_NOMEM;
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+    for (int i = 0; e == hipSuccess && i < 2 * DFS_T_COUNT; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e != hipSuccess) {
+        dfs_close(c);
+        return hip_fail(e, "dfs_open");
+    }
+    *out = c;
+    return DFS_OK;
+}
+
+int dfs_close(dfs_ctx* c) {
+    if (!c) return DFS_E_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->own) (void)hipStreamSynchronize(c->own);
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
+    for (auto& b : c->buf) b.release();
+    for (auto& ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    delete c;
+    return DFS_OK;
+}
+
+int dfs_set_stream(dfs_ctx* c, void* s) {
+    if (!c) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->user = static_cast<hipStream_t>(s);
+    return DFS_OK;
+}
+
+int dfs_set_profiling(dfs_ctx* c, int on) {
+    if (!c) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->profiling = on != 0;
+    return DFS_OK;
+}
+
+int dfs_get_timings(dfs_ctx* c, float* ms, int n) {
+    if (!c || !ms) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    for (int k = 0; k < n && k < DFS_T_COUNT; ++k) {
+        ms[k] = -1.0f;
+        if (!c->ev_used[k]) continue;
+        HIPC(hipEventSynchronize(c->ev[2 * k + 1]));
+        HIPC(hipEventElapsedTime(&ms[k], c->ev[2 * k], c->ev[2 * k + 1]));
+    }
+    return DFS_OK;
+}
+
+int dfs_split_plan(uint64_t file_len, uint32_t nfrag, dfs_span* frags) {
+    if (!nfrag || !frags) return DFS_E_ARG;
+    for (uint32_t i = 0; i < nfrag; ++i) {
+        const uint64_t base = file_len / nfrag, rem = file_len % nfrag;
+        frags[i].len = base + (i < rem ? 1 : 0);
+        frags[i].off = i * base + (i < rem ? i : rem);
+    }
+    return DFS_OK;
+}
+
+uint64_t dfs_b64_encoded_len(uint64_t n) { return enc_len(n); }
+uint64_t dfs_b64_decoded_cap(uint64_t n) { return 3 * ((n + 3) / 4); }
+
+int dfs_fragment_holders(uint32_t f, uint32_t n, uint32_t holders[2]) {
+    if (!n || f >= n || !holders) return DFS_E_ARG;
+    holders[0] = f;                // nodeA = i+1 (1-based), SN:427
+    holders[1] = (f + n - 1) % n;  // nodeB = ((i-1+N)%N)+1, SN:428
+    return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint32_t n, uint8_t* digests,
+                     uint32_t flags) {
+    if (!c || (n && (!msgs || !digests))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!n) return DFS_OK;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    hipStream_t s = c->stream();
+    std::vector<ShaDesc> d(n);
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (msgs[i].len >= kMaxMsg) return DFS_E_ARG;
+        d[i] = ShaDesc{msgs[i].off, msgs[i].len, i, 0};
+        end = std::max(end, msgs[i].off + msgs[i].len);
+    }
+    if (end && !base) return DFS_E_ARG;
+    const uint32_t prio = sort_lanes(d);
+    const uint8_t* d_base = base;
+    uint8_t* d_dig = digests;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, base, end, s)) return rc;
+        d_base = c->buf[B_DATA_IN].as<uint8_t>();
+        HIPC(c->buf[B_DIG0].ensure(32ull * n));
+        d_dig = c->buf[B_DIG0].as<uint8_t>();
+    }
+    if (int rc = put(c, B_DESC, d.data(), d.size() * sizeof(ShaDesc), s)) return rc;
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_SHA, s);
+    HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig, nullptr, s));
+    tm.end(DFS_T_SHA, s);
+    tm.end(DFS_T_TOTAL, s);
+    if (!dev) {
+        HIPC(hipMemcpyAsync(digests, d_dig, 32ull * n, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint32_t n, char* out,
+                         uint64_t out_cap, uint64_t* out_off, uint32_t flags) {
+    if (!c || !out_off || (n && !msgs)) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    hipStream_t s = c->stream();
+    uint64_t total = 0, end = 0;
+    std::vector<StreamJob> jobs;
+    std::vector<uint64_t> items;
+    for (uint32_t i = 0; i < n; ++i) {
+        out_off[i] = total;
+        if (msgs[i].len) {
+            StreamJob j{};
+            j.src_off = msgs[i].off;
+            j.len = msgs[i].len;
+            j.dst_off = total;
+            j.id = i;
+            jobs.push_back(j);
+            items.push_back((msgs[i].len + 11) / 12);
+        }
+        total += enc_len(msgs[i].len);
+        end = std::max(end, msgs[i].off + msgs[i].len);
+    }
+    out_off[n] = total;
+    if (total > out_cap || (total && !out) || (end && !base)) return DFS_E_ARG;
+    const uint32_t njobs = static_cast<uint32_t>(jobs.size());
+    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kEncGroupsPerTile);
+    const uint8_t* d_base = base;
+    char* d_out = out;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, base, end, s)) return rc;
+        d_base = c->buf[B_DATA_IN].as<uint8_t>();
+        HIPC(c->buf[B_DATA_OUT].ensure(total));
+        d_out = c->buf[B_DATA_OUT].as<char>();
+    } else if (reinterpret_cast<uintptr_t>(out) & 3u) {
+        return DFS_E_ARG;
+    }
+    if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_B64ENC, s);
+    HIPC(dfs::launch_b64_encode(d_base, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s));
+    tm.end(DFS_T_B64ENC, s);
+    tm.end(DFS_T_TOTAL, s);
+    if (!dev) {
+        if (total) HIPC(hipMemcpyAsync(out, d_out, total, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint32_t n, uint8_t* out,
+                         const uint64_t* out_off, uint64_t* out_len, int32_t* status, uint32_t flags) {
+    if (!c || (n && (!msgs || !out_off || !out_len || !status))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!n) return DFS_OK;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    hipStream_t s = c->stream();
+    uint64_t in_end = 0, out_end = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        in_end = std::max(in_end, msgs[i].off + msgs[i].len);
+        out_end = std::max(out_end, out_off[i] + dfs_b64_decoded_cap(msgs[i].len));
+    }
+    if ((in_end && !in) || (out_end && !out)) return DFS_E_ARG;
+    const char* d_in = in;
+    uint8_t* d_out = out;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, in, in_end, s)) return rc;
+        d_in = c->buf[B_DATA_IN].as<char>();
+        HIPC(c->buf[B_DATA_OUT].ensure(out_end));
+        d_out = c->buf[B_DATA_OUT].as<uint8_t>();
+    }
+    std::vector<StreamJob> jobs(n);
+    std::vector<uint64_t> items(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        StreamJob& j = jobs[i];
+        j = StreamJob{};
+        j.src_off = msgs[i].off;
+        j.len = msgs[i].len;
+        j.dst_off = out_off[i];
+        j.id = i;
+        items[i] = dec_items(msgs[i].len, reinterpret_cast<uintptr_t>(d_out + out_off[i]));
+    }
+    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecChunksPerTile);
+    if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
+    HIPC(c->buf[B_STATUS].ensure(4ull * n));
+    HIPC(c->buf[B_OUTLEN].ensure(8ull * n));
+    HIPC(hipMemsetAsync(c->buf[B_STATUS].p, 0, 4ull * n, s));
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_B64DEC, s);
+    HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), n, ntiles, d_out,
+                                c->buf[B_STATUS].as<int32_t>(), c->buf[B_OUTLEN].as<uint64_t>(), s));
+    tm.end(DFS_T_B64DEC, s);
+    tm.end(DFS_T_TOTAL, s);
+    std::vector<int32_t> st(n);
+    HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * n, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(out_len, c->buf[B_OUTLEN].p, 8ull * n, hipMemcpyDeviceToHost, s));
+    if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    int rc = DFS_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        status[i] = st[i] ? DFS_E_DECODE : DFS_OK;
+        if (st[i]) {
+            out_len[i] = 0;
+            rc = DFS_E_DECODE;
+        }
+    }
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Upload plan: descriptors built once on the host, uploaded once.
+int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, uint32_t nfrag,
+                           dfs_upload_plan** out, uint64_t* b64_total) {
+    if (!c || !out || !nfrag || (nfiles && !files)) return DFS_E_ARG;
+    *out = nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    auto* p = new (std::nothrow) dfs_upload_plan;
+    if (!p) return DFS_E_NOMEM;
+    p->device = c->device;
+    p->nfiles = nfiles;
+    p->nfrag = nfrag;
+    const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
+    if (nfiles + nf > 0xffffffffull) {
+        delete p;
+        return DFS_E_ARG;
+    }
+    std::vector<ShaDesc> all, frag;
+    all.reserve(nfiles + nf);
+    frag.reserve(nf);
+    std::vector<StreamJob> enc;
+    std::vector<uint64_t> items;
+    enc.reserve(nf + 1);
+    items.reserve(nf);
+    p->b64_off.resize(nf + 1);
+    std::vector<uint64_t> off(nfrag), len(nfrag);
+    uint64_t total = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        if (files[f].len >= kMaxMsg) {
+            delete p;
+            return DFS_E_ARG;
+        }
+        all.push_back(ShaDesc{files[f].off, files[f].len, f, 0});  // fileId, SN:127
+        split(files[f].len, nfrag, off.data(), len.data());          // SN:138-157
+        for (uint32_t i = 0; i < nfrag; ++i) {
+            const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+            const ShaDesc d{files[f].off + off[i], len[i], static_cast<uint32_t>(nfiles + k), 0};  // SN:159
+            all.push_back(d);
+            frag.push_back(d);
+            p->b64_off[k] = total;
+            if (len[i]) {
+                StreamJob j{};
+                j.src_off = files[f].off + off[i];
+                j.len = len[i];
+                j.dst_off = total;
+                j.id = static_cast<uint32_t>(k);
+                enc.push_back(j);
+                items.push_back((len[i] + 11) / 12);
+            }
+            total += enc_len(len[i]);  // SN:636
+        }
+    }
+    p->b64_off[nf] = total;
+    p->b64_total = total;
+    p->prio_all = sort_lanes(all);
+    p->prio_frag = sort_lanes(frag);
+    p->n_all = static_cast<uint32_t>(all.size());
+    p->n_frag_only = static_cast<uint32_t>(frag.size());
+    p->n_enc = static_cast<uint32_t>(enc.size());
+    p->enc_tiles = finish_jobs(enc, items, dfs::kEncGroupsPerTile);
+    hipError_t e = hipMalloc(&p->d_all, std::max<size_t>(all.size(), 1) * sizeof(ShaDesc));
+    if (e == hipSuccess) e = hipMalloc(&p->d_frag, std::max<size_t>(frag.size(), 1) * sizeof(ShaDesc));
+    if (e == hipSuccess) e = hipMalloc(&p->d_enc, enc.size() * sizeof(StreamJob));
+    if (e == hipSuccess && !all.empty())
+        e = hipMemcpy(p->d_all, all.data(), all.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !frag.empty())
+        e = hipMemcpy(p->d_frag, frag.data(), frag.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(p->d_enc, enc.data(), enc.size() * sizeof(StreamJob), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        dfs_upload_plan_destroy(p);
+        return hip_fail(e, "dfs_upload_plan_create");
+    }
+    if (b64_total) *b64_total = total;
+    *out = p;
+    return DFS_OK;
+}
+
+int dfs_upload_plan_b64_offsets(const dfs_upload_plan* p, uint64_t* b64_off) {
+    if (!p || !b64_off) return DFS_E_ARG;
+    std::memcpy(b64_off, p->b64_off.data(), p->b64_off.size() * sizeof(uint64_t));
+    return DFS_OK;
+}
+
+int dfs_upload_plan_destroy(dfs_upload_plan* p) {
+    if (!p) return DFS_E_ARG;
+    (void)hipSetDevice(p->device);
+    if (p->d_all) (void)hipFree(p->d_all);
+    if (p->d_frag) (void)hipFree(p->d_frag);
+    if (p->d_enc) (void)hipFree(p->d_enc);
+    delete p;
+    return DFS_OK;
+}
+
+namespace {
+int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint8_t* d_fd, uint8_t* d_frd, char* d_b64,
+                    uint32_t flags) {
+    const bool do_fileid = !(flags & DFS_NO_FILEID);
+    const bool do_b64 = !(flags & DFS_NO_B64) && p->n_enc;
+    const bool serial = flags & DFS_SERIAL;
+    if (!d_frd || (do_fileid && !d_fd) || (do_b64 && !d_b64)) return DFS_E_ARG;
+    if (do_b64 && (reinterpret_cast<uintptr_t>(d_b64) & 3u)) return DFS_E_ARG;
+    hipStream_t s = c->stream();
+    hipStream_t sb = serial ? s : c->aux;
+    Timer tm(c);
+    tm.begin(DFS_T_TOTAL, s);
+    if (do_b64 && !serial) {  // fork: Base64 on the aux stream beside SHA
+        HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER], s));
+        HIPC(hipStreamWaitEvent(sb, c->ev[2 * DFS_T_GATHER], 0));
+    }
+    tm.begin(DFS_T_SHA, s);
+    if (do_fileid) {
+        // out index < nfiles -> file digest, else fragment digest (split = nfiles)
+        HIPC(dfs::launch_sha256(d_files, p->d_all, p->n_all, p->nfiles, p->prio_all, d_fd, d_frd, nullptr, s));
+    } else {
+        HIPC(dfs::launch_sha256(d_files, p->d_frag, p->n_frag_only, p->nfiles, p->prio_frag, d_fd, d_frd, nullptr,
+                                s));
+    }
+    tm.end(DFS_T_SHA, s);
+    if (do_b64) {
+        tm.begin(DFS_T_B64ENC, sb);
+        HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64, sb));
+        tm.end(DFS_T_B64ENC, sb);
+        if (!serial) {  // join
+            HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER + 1], sb));
+            HIPC(hipStreamWaitEvent(s, c->ev[2 * DFS_T_GATHER + 1], 0));
+        }
+    }
+    tm.end(DFS_T_TOTAL, s);
+    return DFS_OK;
+}
+}  // namespace
+
+int dfs_upload_plan_run(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint8_t* d_fd, uint8_t* d_frd,
+                        char* d_b64, uint32_t flags) {
+    if (!c || !p || p->device != c->device) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    return run_plan_locked(c, p, d_files, d_fd, d_frd, d_b64, flags);
+}
+
+int dfs_upload_batch(dfs_ctx* c, const uint8_t* files, const dfs_span* spans, uint32_t nfiles, uint32_t nfrag,
+                     uint8_t* fd, uint8_t* frd, char* b64, uint64_t b64_cap, uint64_t* b64_off, uint32_t flags) {
+    if (!c || !nfrag || (nfiles && (!spans || !frd))) return DFS_E_ARG;
+    if (!(flags & DFS_NO_FILEID) && nfiles && !fd) return DFS_E_ARG;
+    dfs_upload_plan* p = nullptr;
+    uint64_t total = 0;
+    if (int rc = dfs_upload_plan_create(c, spans, nfiles, nfrag, &p, &total)) return rc;
+    struct Guard {
+        dfs_upload_plan* p;
+        ~Guard() { dfs_upload_plan_destroy(p); }
+    } guard{p};
+    const bool do_b64 = !(flags & DFS_NO_B64);
+    if (b64_off) std::memcpy(b64_off, p->b64_off.data(), p->b64_off.size() * sizeof(uint64_t));
+    if (do_b64 && (total > b64_cap || (total && !b64))) return DFS_E_ARG;
+    if (!nfiles) return DFS_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    hipStream_t s = c->stream();
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    uint64_t end = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) end = std::max(end, spans[f].off + spans[f].len);
+    if (end && !files) return DFS_E_ARG;
+    const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
+    const uint8_t* d_files = files;
+    uint8_t* d_fd = fd;
+    uint8_t* d_frd = frd;
+    char* d_b64 = b64;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, files, end, s)) return rc;
+        d_files = c->buf[B_DATA_IN].as<uint8_t>();
+        HIPC(c->buf[B_DIG0].ensure(32ull * nfiles));
+        HIPC(c->buf[B_DIG1].ensure(32ull * nf));
+        d_fd = c->buf[B_DIG0].as<uint8_t>();
+        d_frd = c->buf[B_DIG1].as<uint8_t>();
+        if (do_b64) {
+            HIPC(c->buf[B_DATA_OUT].ensure(total));
+            d_b64 = c->buf[B_DATA_OUT].as<char>();
+        }
+    }
+    if (int rc = run_plan_locked(c, p, d_files, d_fd, d_frd, d_b64, flags)) return rc;
+    if (!dev) {
+        if (!(flags & DFS_NO_FILEID)) HIPC(hipMemcpyAsync(fd, d_fd, 32ull * nfiles, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(frd, d_frd, 32ull * nf, hipMemcpyDeviceToHost, s));
+        if (do_b64 && total) HIPC(hipMemcpyAsync(b64, d_b64, total, hipMemcpyDeviceToHost, s));
+    }
+    HIPC(hipStreamSynchronize(s));  // the plan is freed on return
+    return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t* frag_len, uint32_t nfiles,
+                          uint32_t nfrag, uint8_t* out, const uint64_t* file_off, const uint8_t* expected,
+                          uint8_t* digest_out, int32_t* status, uint32_t flags) {
+    if (!c || !nfrag || (nfiles && (!src || !frag_len || !out || !file_off || !status))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!nfiles) return DFS_OK;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    hipStream_t s = c->stream();
+    const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
+    std::vector<uint64_t> flen(nfiles, 0);
+    uint64_t out_end = 0, stage = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        status[f] = DFS_OK;
+        for (uint32_t i = 0; i < nfrag; ++i) {
+            const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+            if (!src[k] && frag_len[k]) status[f] = DFS_E_MISSING;  // SN:443-446
+            flen[f] += frag_len[k];
+            stage += frag_len[k];
+        }
+        out_end = std::max(out_end, file_off[f] + flen[f]);
+    }
+    uint8_t* d_out = out;
+    std::vector<uint64_t> src_addr(nf, 0);
+    if (!dev) {
+        // Stage every host fragment contiguously on the device.
+        HIPC(c->buf[B_DATA_IN].ensure(stage));
+        HIPC(c->buf[B_DATA_OUT].ensure(out_end));
+        d_out = c->buf[B_DATA_OUT].as<uint8_t>();
+        uint64_t o = 0;
+        for (uint64_t k = 0; k < nf; ++k) {
+            if (!src[k] || !frag_len[k]) continue;
+            HIPC(hipMemcpyAsync(c->buf[B_DATA_IN].as<uint8_t>() + o, src[k], frag_len[k], hipMemcpyHostToDevice, s));
+            src_addr[k] = reinterpret_cast<uint64_t>(c->buf[B_DATA_IN].as<uint8_t>() + o);
+            o += frag_len[k];
+        }
+    } else {
+        for (uint64_t k = 0; k < nf; ++k) src_addr[k] = reinterpret_cast<uint64_t>(src[k]);
+    }
+    std::vector<StreamJob> jobs;
+    std::vector<uint64_t> items;
+    std::vector<ShaDesc> sha;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        if (status[f] != DFS_OK) continue;
+        uint64_t o = file_off[f];
+        for (uint32_t i = 0; i < nfrag; ++i) {
+            const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+            if (frag_len[k]) {
+                StreamJob j{};
+                j.src_off = src_addr[k];
+                j.len = frag_len[k];
+                j.dst_off = o;  // ordered append, SN:448
+                j.id = static_cast<uint32_t>(k);
+                jobs.push_back(j);
+                items.push_back(copy_items(frag_len[k], reinterpret_cast<uintptr_t>(d_out + o)));
+            }
+            o += frag_len[k];
+        }
+        sha.push_back(ShaDesc{file_off[f], flen[f], f, 0});  // SN:454
+    }
+    const uint32_t njobs = static_cast<uint32_t>(jobs.size());
+    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kCopyChunksPerTile);
+    const uint32_t prio = sort_lanes(sha);
+    if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
+    if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
+    HIPC(c->buf[B_DIG0].ensure(32ull * nfiles));
+    uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_GATHER, s);
+    HIPC(dfs::launch_gather(c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s));
+    tm.end(DFS_T_GATHER, s);
+    tm.begin(DFS_T_SHA, s);
+    HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
+                            d_dig, d_dig, nullptr, s));
+    tm.end(DFS_T_SHA, s);
+    tm.end(DFS_T_TOTAL, s);
+    std::vector<uint8_t> dig(32ull * nfiles);
+    HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+    if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    int rc = DFS_OK;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        if (status[f] == DFS_OK && expected && std::memcmp(dig.data() + 32ull * f, expected + 32ull * f, 32) != 0)
+            status[f] = DFS_E_CORRUPT;  // SN:455-458
+        if (digest_out) std::memcpy(digest_out + 32ull * f, dig.data() + 32ull * f, 32);
+        if (status[f] != DFS_OK && rc == DFS_OK) rc = status[f];
+    }
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32_t nfiles, uint32_t nfrag,
+                       const uint64_t* file_len, const uint8_t* exp_frag, const uint8_t* exp_file, uint8_t* out,
+                       const uint64_t* file_off, int32_t* status, uint32_t flags) {
+    if (!c || !nfrag || (nfiles && (!msgs || !file_len || !out || !file_off || !status))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!nfiles) return DFS_OK;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    hipStream_t s = c->stream();
+    const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
+    uint64_t in_end = 0, out_end = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        status[f] = DFS_OK;
+        if (file_len[f] >= kMaxMsg) return DFS_E_ARG;
+        out_end = std::max(out_end, file_off[f] + file_len[f]);
+        for (uint32_t i = 0; i < nfrag; ++i) {
+            const dfs_span& m = msgs[static_cast<uint64_t>(f) * nfrag + i];
+            if (m.len == DFS_SPAN_MISSING) status[f] = DFS_E_MISSING;  // SN:443-446
+            else in_end = std::max(in_end, m.off + m.len);
+        }
+    }
+    if ((in_end && !b64) || (out_end && !out)) return DFS_E_ARG;
+    const char* d_in = b64;
+    uint8_t* d_out = out;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, b64, in_end, s)) return rc;
+        d_in = c->buf[B_DATA_IN].as<char>();
+        HIPC(c->buf[B_DATA_OUT].ensure(out_end));
+        d_out = c->buf[B_DATA_OUT].as<uint8_t>();
+    }
+    // Decode jobs write straight into the file at the split offsets (fused gather).
+    std::vector<StreamJob> jobs;
+    std::vector<uint64_t> items;
+    std::vector<ShaDesc> sha;  // fragments (out = k) then files (out = nf + f)
+    std::vector<uint64_t> off(nfrag), len(nfrag);
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        if (status[f] != DFS_OK) continue;
+        split(file_len[f], nfrag, off.data(), len.data());
+        for (uint32_t i = 0; i < nfrag; ++i) {
+            const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+            StreamJob j{};
+            j.src_off = msgs[k].off;
+            j.len = msgs[k].len;
+            j.dst_off = file_off[f] + off[i];
+            j.expect = len[i] + 1;
+            j.id = static_cast<uint32_t>(k);
+            jobs.push_back(j);
+            items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
+            sha.push_back(ShaDesc{file_off[f] + off[i], len[i], static_cast<uint32_t>(k), 0});
+        }
+        sha.push_back(ShaDesc{file_off[f], file_len[f], static_cast<uint32_t>(nf + f), 0});
+    }
+    const uint32_t njobs = static_cast<uint32_t>(jobs.size());
+    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecChunksPerTile);
+    const uint32_t prio = sort_lanes(sha);
+    if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
+    if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
+    HIPC(c->buf[B_STATUS].ensure(4ull * nf));
+    HIPC(c->buf[B_DIG0].ensure(32ull * (nf + nfiles)));
+    HIPC(hipMemsetAsync(c->buf[B_STATUS].p, 0, 4ull * nf, s));
+    uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_B64DEC, s);
+    HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out,
+                                c->buf[B_STATUS].as<int32_t>(), nullptr, s));
+    tm.end(DFS_T_B64DEC, s);
+    tm.begin(DFS_T_SHA, s);
+    HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
+                            static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig, nullptr, s));
+    tm.end(DFS_T_SHA, s);
+    tm.end(DFS_T_TOTAL, s);
+    std::vector<int32_t> st(nf);
+    std::vector<uint8_t> dig(32ull * (nf + nfiles));
+    HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * nf, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+    if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    std::vector<uint8_t> expf, expd;
+    if (dev && exp_frag) {  // expected digests may be device pointers in device mode
+        expf.resize(32ull * nf);
+        HIPC(hipMemcpy(expf.data(), exp_frag, expf.size(), hipMemcpyDefault));
+        exp_frag = expf.data();
+    }
+    if (dev && exp_file) {
+        expd.resize(32ull * nfiles);
+        HIPC(hipMemcpy(expd.data(), exp_file, expd.size(), hipMemcpyDefault));
+        exp_file = expd.data();
+    }
+    int rc = DFS_OK;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        if (status[f] == DFS_OK) {
+            for (uint32_t i = 0; i < nfrag && status[f] == DFS_OK; ++i)
+                if (st[static_cast<uint64_t>(f) * nfrag + i]) status[f] = DFS_E_DECODE;  // SN:281 IAE
+            for (uint32_t i = 0; i < nfrag && status[f] == DFS_OK && exp_frag; ++i) {
+                const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+                if (std::memcmp(dig.data() + 32 * k, exp_frag + 32 * k, 32) != 0)
+                    status[f] = DFS_E_FRAG_MISMATCH;  // SN:250-257
+            }
+            if (status[f] == DFS_OK && exp_file &&
+                std::memcmp(dig.data() + 32 * (nf + f), exp_file + 32ull * f, 32) != 0)
+                status[f] = DFS_E_CORRUPT;  // SN:454-458
+        }
+        if (status[f] != DFS_OK && rc == DFS_OK) rc = status[f];
+    }
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_synth_fill(dfs_ctx* c, uint8_t* d_dst, const dfs_span* files, uint32_t nfiles, uint64_t first, uint64_t seed) {
+    if (!c || (nfiles && (!files || !d_dst))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    if (!nfiles) return DFS_OK;
+    hipStream_t s = c->stream();
+    std::vector<StreamJob> jobs;
+    std::vector<uint64_t> items;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        if (!files[f].len) continue;
+        StreamJob j{};
+        j.src_off = first + f;
+        j.len = files[f].len;
+        j.dst_off = files[f].off;
+        jobs.push_back(j);
+        items.push_back((files[f].len + 63) / 64);
+    }
+    const uint32_t njobs = static_cast<uint32_t>(jobs.size());
+    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kStreamBlock);
+    if (int rc = put(c, B_JOBS2, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
+    HIPC(dfs::launch_synth(d_dst, c->buf[B_JOBS2].as<StreamJob>(), njobs, ntiles, seed, s));
+    HIPC(hipStreamSynchronize(s));  // the job table lives in reusable scratch
+    return DFS_OK;
+}
+
+}  // extern "C"

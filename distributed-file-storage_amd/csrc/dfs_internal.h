@@ -1,0 +1,65 @@
+// dfs_internal.h — device-side job descriptors and kernel launchers shared by
+// the HIP kernels (sha256.hip, base64.hip, gather.hip) and the C ABI
+// (dfs_gpu.cpp).  Not part of the public boundary (include/dfs_gpu.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dfs {
+
+// One SHA-256 lane: message bytes [off, off+len) of the batch buffer; the
+// digest goes to out0 + 32*out (out < split) or out1 + 32*(out - split).
+struct ShaDesc {
+    uint64_t off;
+    uint64_t len;
+    uint32_t out;
+    uint32_t pad;
+};
+
+// One byte-stream job for the tiled HBM-bound kernels (Base64 encode/decode,
+// gather, synth).  Jobs are sorted by tile_start; a sentinel job with
+// tile_start = total tiles ends the array.
+struct StreamJob {
+    uint64_t src_off;     // input byte offset (or absolute address for gather)
+    uint64_t len;         // input length (bytes or chars)
+    uint64_t dst_off;     // output byte offset
+    uint64_t tile_start;  // first tile index of this job
+    uint64_t expect;      // decode: expected decoded length + 1 (0 = any)
+    uint32_t id;          // message index (status / out_len slot)
+    uint32_t aux;         // kernel-specific (synth: unused)
+};
+
+constexpr int kShaBlock = 256;       // threads per SHA workgroup (4 waves)
+constexpr int kStreamBlock = 256;    // threads per stream workgroup
+constexpr int kEncGroupsPerTile = 1024;  // 12-byte groups (4 per thread)
+constexpr int kDecChunksPerTile = 1024;  // 12-byte output chunks (4 per thread)
+constexpr int kCopyChunksPerTile = 1024; // 16-byte output chunks (4 per thread)
+
+// Tiles per job.
+inline uint64_t enc_tiles(uint64_t len) {
+    uint64_t groups = (len + 11) / 12;
+    return (groups + kEncGroupsPerTile - 1) / kEncGroupsPerTile;
+}
+
+// Launchers (return hipError_t of the launch).
+hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
+                         uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* census,
+                         hipStream_t s);
+hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
+                             char* out, hipStream_t s);
+// Decode: chars of job j at in + src_off decode to out + dst_off.
+// status[id] |= 1 on an IllegalArgumentException case; out_len[id] = bytes.
+// If job.expect != 0 it is the expected decoded length + 1 (download path):
+// a different length sets status bit 2.
+hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
+                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s);
+// Gather: job.src_off is an absolute device address of the fragment.
+hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
+                         hipStream_t s);
+hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
+                        uint64_t seed, hipStream_t s);
+// Compare n digests a[i] vs b[i] (32 B each); status[i*stride] = code if different.
+hipError_t launch_digest_compare(const uint8_t* a, const uint8_t* b, uint32_t n, int32_t code,
+                                 int32_t* status, uint32_t status_div, hipStream_t s);
+
+}  // namespace dfs

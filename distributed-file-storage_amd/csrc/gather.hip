@@ -1,0 +1,128 @@
+// gather.hip — reassembly gather, synthetic data and digest compare.
+//
+// gather_kernel replaces handleDownload's ordered reassembly
+// (ByteArrayOutputStream.write at StorageNode.java:448, toByteArray at :451):
+// fragment i of file f is copied to file_off[f] + off_i (the split offsets
+// of :138-157).  HBM-bound: every destination dword is written once by an
+// aligned store; misaligned sources are funnel-shifted in registers.
+#include "stream_common.h"
+
+namespace dfs {
+namespace {
+
+__global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* __restrict__ jobs, uint32_t njobs,
+                                                              uint64_t ntiles, uint8_t* __restrict__ out) {
+    uint64_t t0, t1;
+    tile_range(ntiles, t0, t1);
+    if (t0 >= t1) return;
+    uint32_t j = find_job(jobs, njobs, t0);
+    for (uint64_t t = t0; t < t1; ++t) {
+        while (jobs[j + 1].tile_start <= t) ++j;
+        const uint64_t len = jobs[j].len;
+        const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(jobs[j].src_off);
+        uint8_t* __restrict__ dst = out + jobs[j].dst_off;
+        const uint32_t h = static_cast<uint32_t>((4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u);
+        const uint64_t nc = len > h ? (len - h) / 16 : 0;
+        const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src + h)) & 3u;
+        const uint64_t c0 = (t - jobs[j].tile_start) * kCopyChunksPerTile + threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < kCopyChunksPerTile / kStreamBlock; ++i) {
+            const uint64_t c = c0 + static_cast<uint64_t>(i) * kStreamBlock;
+            if (c < nc) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + h + 16 * c - sa);
+                const uint4 v = *reinterpret_cast<const uint4*>(w);
+                uint4 o;
+                if (sa) {
+                    const uint32_t x = w[4];
+                    o.x = __builtin_amdgcn_alignbyte(v.y, v.x, sa);
+                    o.y = __builtin_amdgcn_alignbyte(v.z, v.y, sa);
+                    o.z = __builtin_amdgcn_alignbyte(v.w, v.z, sa);
+                    o.w = __builtin_amdgcn_alignbyte(x, v.w, sa);
+                } else {
+                    o = v;
+                }
+                *reinterpret_cast<uint4*>(dst + h + 16 * c) = o;
+            } else if (c == nc) {
+                const uint64_t head_end = h < len ? h : len;
+                for (uint64_t b = 0; b < head_end; ++b) dst[b] = src[b];
+                for (uint64_t b = h + 16 * nc; b < len; ++b) dst[b] = src[b];
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// Synthetic files: job.src_off = file index, job.len = bytes, job.dst_off.
+// Item c covers file bytes [64c, 64c+64).
+__global__ __launch_bounds__(kStreamBlock) void synth_kernel(uint8_t* __restrict__ dst_base,
+                                                             const StreamJob* __restrict__ jobs, uint32_t njobs,
+                                                             uint64_t ntiles, uint64_t seed) {
+    uint64_t t0, t1;
+    tile_range(ntiles, t0, t1);
+    if (t0 >= t1) return;
+    uint32_t j = find_job(jobs, njobs, t0);
+    for (uint64_t t = t0; t < t1; ++t) {
+        while (jobs[j + 1].tile_start <= t) ++j;
+        const uint64_t f = jobs[j].src_off, len = jobs[j].len;
+        uint8_t* __restrict__ dst = dst_base + jobs[j].dst_off;
+        const bool aligned = (reinterpret_cast<uintptr_t>(dst) & 7u) == 0;
+        const uint64_t c = (t - jobs[j].tile_start) * kStreamBlock + threadIdx.x;
+        const uint64_t b0 = 64 * c;
+        if (b0 >= len) continue;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint64_t o = b0 + 8 * k;
+            if (o >= len) break;
+            const uint64_t v = splitmix64(seed ^ ((f << 40) | (o >> 3)));
+            if (aligned && o + 8 <= len) {
+                *reinterpret_cast<uint64_t*>(dst + o) = v;
+            } else {
+                for (uint64_t b = o; b < o + 8 && b < len; ++b) dst[b] = static_cast<uint8_t>(v >> (8 * (b & 7)));
+            }
+        }
+    }
+}
+
+__global__ void digest_compare_kernel(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, uint32_t n,
+                                      int32_t code, int32_t* __restrict__ status, uint32_t status_div) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4* x = reinterpret_cast<const uint4*>(a + 32ull * i);
+    const uint4* y = reinterpret_cast<const uint4*>(b + 32ull * i);
+    const uint4 x0 = x[0], x1 = x[1], y0 = y[0], y1 = y[1];
+    const uint32_t d = (x0.x ^ y0.x) | (x0.y ^ y0.y) | (x0.z ^ y0.z) | (x0.w ^ y0.w) | (x1.x ^ y1.x) |
+                       (x1.y ^ y1.y) | (x1.z ^ y1.z) | (x1.w ^ y1.w);
+    if (d) atomicOr(status + i / status_div, code);
+}
+
+}  // namespace
+
+hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
+                        hipStream_t s) {
+    if (ntiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(synth_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, dst, jobs, njobs, ntiles,
+                       seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_digest_compare(const uint8_t* a, const uint8_t* b, uint32_t n, int32_t code, int32_t* status,
+                                 uint32_t status_div, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(digest_compare_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, b, n, code, status,
+                       status_div);
+    return hipGetLastError();
+}
+
+}  // namespace dfs

@@ -1,0 +1,196 @@
+// sha256.hip — multi-message SHA-256 for gfx950 (MI355X).
+//
+// Replaces MessageDigest.getInstance("SHA-256").digest(...) at every
+// sha256Hex call site of StorageNode.java (SN:127 fileId, SN:159 fragment,
+// SN:282 received fragment, SN:454 download verify).  FIPS 180-4.
+//
+// Design:
+//  * One message per lane.  SHA-256 is a strict chain within a message, so
+//    the parallelism is across messages (files' fragments and fileIds).
+//  * Lanes are pre-sorted by length (longest first) on the host so waves are
+//    uniform; the waves that carry the longest chains (fileIds) raise their
+//    issue priority (s_setprio) because they are the critical path.
+//  * Int-VALU bound: 64 rounds are fully unrolled; rotations are
+//    v_alignbit_b32, the three-input XORs / Ch / Maj are single
+//    v_bitop3_b32 ops (gfx950), additions fold into v_add3_u32.
+//  * Arbitrary byte offsets (fragment starts are not aligned): each lane
+//    loads 16 aligned dwords + 1 look-ahead dword per block and one
+//    v_perm_b32 per word does the funnel shift and the big-endian swap.
+//  * The next block is prefetched into a second register set while the
+//    current one is compressed (two register buffers, loop unrolled x2).
+#include "dfs_internal.h"
+
+namespace dfs {
+namespace {
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t bsig0(uint32_t a) { return xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)); }
+__device__ __forceinline__ uint32_t bsig1(uint32_t e) { return xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)); }
+__device__ __forceinline__ uint32_t ssig0(uint32_t x) { return xor3(rotr(x, 7), rotr(x, 18), x >> 3); }
+__device__ __forceinline__ uint32_t ssig1(uint32_t x) { return xor3(rotr(x, 17), rotr(x, 19), x >> 10); }
+// Ch(e,f,g) = e ? f : g  (truth table 0xCA);  Maj(a,b,c) (0xE8).
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+    return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+
+constexpr uint32_t kK[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+// FIPS 180-4 §6.2.2 compression of one 64-byte block W (big-endian words).
+// The empty volatile asm statements are ordering points (they emit nothing):
+// each schedule word W[t] (t >= 16) is pinned to round t, so the compiler
+// cannot hoist the whole 48-word message expansion ahead of the rounds
+// (which costs ~30 VGPRs and drops occupancy from 6 to 4 waves/SIMD).
+__device__ __forceinline__ void compress(uint32_t (&st)[8], uint32_t (&W)[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+        if (t >= 16) {
+            W[t & 15] += ssig1(W[(t - 2) & 15]) + W[(t - 7) & 15] + ssig0(W[(t - 15) & 15]);
+            asm volatile("" : "+v"(W[t & 15]));
+        }
+        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kK[t] + W[t & 15];
+        const uint32_t t2 = bsig0(a) + maj(a, b, c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + t2;
+        asm volatile("" : "+v"(a), "+v"(e));
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// 16 words of block k plus the look-ahead word (first word of block k+1),
+// which the unaligned funnel needs for the block's last word.
+__device__ __forceinline__ void load_block(const uint32_t* __restrict__ p, uint32_t sh, uint32_t (&r)[16],
+                                           uint32_t& x) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 v = q[i];
+        r[4 * i + 0] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
+    }
+    x = sh ? p[16] : 0u;
+}
+
+// In place: r[j] <- big-endian word at byte offset sh of {r[j], r[j+1]}.
+__device__ __forceinline__ void to_be(uint32_t (&r)[16], uint32_t x, uint32_t sel) {
+#pragma unroll
+    for (int j = 0; j < 15; ++j) r[j] = __builtin_amdgcn_perm(r[j + 1], r[j], sel);
+    r[15] = __builtin_amdgcn_perm(x, r[15], sel);
+}
+
+__device__ __forceinline__ uint32_t hw_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v;
+}
+
+__global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restrict__ base,
+                                                          const ShaDesc* __restrict__ descs, uint32_t n,
+                                                          uint32_t split, uint32_t prio_lanes,
+                                                          uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
+                                                          uint32_t* __restrict__ census) {
+    const uint32_t gid = blockIdx.x * kShaBlock + threadIdx.x;
+    const uint32_t wave_first = __builtin_amdgcn_readfirstlane(blockIdx.x * kShaBlock + (threadIdx.x & ~63u));
+    if (wave_first < prio_lanes) __builtin_amdgcn_s_setprio(2);
+    const uint32_t wave_index = wave_first >> 6;
+    uint64_t t_start = 0;
+    if (census) t_start = __builtin_amdgcn_s_memrealtime();
+    if (gid < n) {
+        const ShaDesc d = descs[gid];
+        const uint32_t sh = static_cast<uint32_t>(d.off) & 3u;
+        const uint32_t* __restrict__ p = reinterpret_cast<const uint32_t*>(base + (d.off - sh));
+        const uint32_t sel = (sh + 3u) | ((sh + 2u) << 8) | ((sh + 1u) << 16) | (sh << 24);
+        const uint32_t nfull = static_cast<uint32_t>(d.len >> 6);
+        uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                          0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+        if (nfull) {
+            uint32_t A[16], B[16], xa, xb;
+            load_block(p, sh, A, xa);
+            uint32_t k = 0;
+            for (;;) {
+                // A holds block k; prefetch block k+1 (clamped) into B.
+                load_block(p + 16u * min(k + 1u, nfull - 1u), sh, B, xb);
+                to_be(A, xa, sel);
+                compress(st, A);
+                if (++k >= nfull) break;
+                load_block(p + 16u * min(k + 1u, nfull - 1u), sh, A, xa);
+                to_be(B, xb, sel);
+                compress(st, B);
+                if (++k >= nfull) break;
+            }
+        }
+        // Tail: r = len mod 64 bytes + FIPS 180-4 §5.1.1 padding, 1 or 2 blocks.
+        const uint32_t r = static_cast<uint32_t>(d.len) & 63u;
+        const uint64_t bits = d.len << 3;
+        const uint32_t ntb = r < 56u ? 1u : 2u;
+        const uint32_t lim = d.len ? sh + r : 0u;  // word i of the tail holds message bytes iff 4i < lim
+        const uint32_t* __restrict__ q = p + 16u * nfull;
+        for (uint32_t tb = 0; tb < ntb; ++tb) {
+            uint32_t T[17], W[16];
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const uint32_t wi = 16u * tb + static_cast<uint32_t>(i);
+                T[i] = (4u * wi < lim) ? q[wi] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int rem = static_cast<int>(r) - 64 * static_cast<int>(tb) - 4 * j;  // message bytes in word j
+                const uint32_t w = __builtin_amdgcn_perm(T[j + 1], T[j], sel);
+                const uint32_t mask = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
+                const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
+                W[j] = (w & mask) | pad;
+            }
+            if (tb + 1u == ntb) {
+                W[14] = static_cast<uint32_t>(bits >> 32);
+                W[15] = static_cast<uint32_t>(bits);
+            }
+            compress(st, W);
+        }
+        uint8_t* dst = d.out < split ? out0 + 32ull * d.out : out1 + 32ull * (d.out - split);
+        uint4* o = reinterpret_cast<uint4*>(dst);
+        o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                          __builtin_bswap32(st[3]));
+        o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                          __builtin_bswap32(st[7]));
+    }
+    if (census && (threadIdx.x & 63u) == 0u) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t* c = census + 4ull * wave_index;
+        c[0] = hw_id();
+        c[1] = xcc_id();
+        c[2] = static_cast<uint32_t>(t_start);
+        c[3] = static_cast<uint32_t>(t_end);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
+                         uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t grid = (n + kShaBlock - 1) / kShaBlock;
+    hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, prio_lanes, out0,
+                       out1, census);
+    return hipGetLastError();
+}
+
+}  // namespace dfs

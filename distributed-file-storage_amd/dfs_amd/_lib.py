@@ -1,0 +1,104 @@
+"""ctypes binding of libdfsgpu.so (include/dfs_gpu.h).
+
+The library is built in-tree (``make -C distributed-file-storage_amd``) and is
+the only implementation of the data path: there is no Python or CPU fallback.
+Importing this module without the built library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libdfsgpu.so")
+REPO_ROOT = os.path.dirname(PKG_DIR)
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "dfs_gpu.h")
+
+# Return codes / flags (mirrors include/dfs_gpu.h).
+DFS_OK = 0
+DFS_E_ARG = -1
+DFS_E_HIP = -2
+DFS_E_NOMEM = -3
+DFS_E_DECODE = -4
+DFS_E_MISSING = -5
+DFS_E_CORRUPT = -6
+DFS_E_FRAG_MISMATCH = -7
+DFS_E_NODEV = -8
+
+DFS_DEVICE_PTRS = 0x1
+DFS_NO_FILEID = 0x2
+DFS_NO_B64 = 0x4
+DFS_SERIAL = 0x8
+
+DFS_SPAN_MISSING = (1 << 64) - 1
+
+DFS_T_SHA, DFS_T_B64ENC, DFS_T_B64DEC, DFS_T_GATHER, DFS_T_TOTAL, DFS_T_COUNT = range(6)
+
+
+class dfs_span(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint64)]
+
+
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+_int = ctypes.c_int
+
+# name -> (restype, argtypes); every symbol include/dfs_gpu.h declares.
+SIGNATURES = {
+    "dfs_open": (_int, [ctypes.POINTER(_vp), _int]),
+    "dfs_close": (_int, [_vp]),
+    "dfs_strerror": (ctypes.c_char_p, [_int]),
+    "dfs_abi_version": (_int, []),
+    "dfs_set_stream": (_int, [_vp, _vp]),
+    "dfs_set_profiling": (_int, [_vp, _int]),
+    "dfs_get_timings": (_int, [_vp, _vp, _int]),
+    "dfs_split_plan": (_int, [_u64, _u32, _vp]),
+    "dfs_b64_encoded_len": (_u64, [_u64]),
+    "dfs_b64_decoded_cap": (_u64, [_u64]),
+    "dfs_fragment_holders": (_int, [_u32, _u32, _vp]),
+    "dfs_sha256_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _u32]),
+    "dfs_b64_encode_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _u64, _vp, _u32]),
+    "dfs_b64_decode_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]),
+    "dfs_upload_batch": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _u32]),
+    "dfs_reassemble_verify": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _u32]),
+    "dfs_download_batch": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    "dfs_upload_plan_create": (_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
+    "dfs_upload_plan_b64_offsets": (_int, [_vp, _vp]),
+    "dfs_upload_plan_run": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    "dfs_upload_plan_destroy": (_int, [_vp]),
+    "dfs_synth_fill": (_int, [_vp, _vp, _vp, _u32, _u64, _u64]),
+}
+
+_LIB = None
+
+
+class DfsError(RuntimeError):
+    """A DFS_E_* return code (RuntimeException in the Java mapping)."""
+
+    def __init__(self, code: int, where: str = ""):
+        self.code = code
+        msg = lib().dfs_strerror(code).decode(errors="replace")
+        super().__init__(f"{where}: {msg} ({code})" if where else f"{msg} ({code})")
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is not built; run `make -C {PKG_DIR}` (hipcc, gfx950). "
+                "There is no CPU fallback for the fragment pipeline.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int, where: str = "") -> int:
+    if rc != DFS_OK:
+        raise DfsError(rc, where)
+    return rc

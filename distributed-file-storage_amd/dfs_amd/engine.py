@@ -1,0 +1,335 @@
+"""Python face of the fragment pipeline over libdfsgpu.so.
+
+Mirrors the reference's fragment-pipeline operations (StorageNode.java, cited
+SN:line) batch-wise; every byte of data-path work runs in the gfx950 kernels
+behind the C ABI.  Host buffers are numpy arrays; device buffers are torch
+tensors (PyTorch is plumbing here: device memory, streams, distributed).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import check, dfs_span, lib
+
+
+class IllegalArgumentException(ValueError):
+    """java.util.Base64.Decoder's IllegalArgumentException (SN:281)."""
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def _pack(messages: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    """Concatenate byte strings into one buffer + span array."""
+    n = len(messages)
+    spans = np.zeros((n, 2), dtype=np.uint64)
+    total = sum(len(m) for m in messages)
+    buf = np.empty(max(total, 1), dtype=np.uint8)
+    o = 0
+    for i, m in enumerate(messages):
+        ln = len(m)
+        spans[i] = (o, ln)
+        if ln:
+            buf[o:o + ln] = np.frombuffer(m, dtype=np.uint8)
+        o += ln
+    return buf, spans
+
+
+def split_plan(file_len: int, nfrag: int) -> List[Tuple[int, int]]:
+    """handleUpload's split (SN:138-171) as computed by the library."""
+    out = (dfs_span * nfrag)()
+    check(lib().dfs_split_plan(file_len, nfrag, out), "dfs_split_plan")
+    return [(s.off, s.len) for s in out]
+
+
+def fragment_holders(frag: int, nfrag: int) -> Tuple[int, int]:
+    """0-based nodes holding fragment `frag` (SN:143-145, 427-428)."""
+    h = (ctypes.c_uint32 * 2)()
+    check(lib().dfs_fragment_holders(frag, nfrag, h), "dfs_fragment_holders")
+    return h[0], h[1]
+
+
+def b64_encoded_len(n: int) -> int:
+    return lib().dfs_b64_encoded_len(n)
+
+
+@dataclass
+class Fragment:
+    """StorageNode.Fragment (SN:779-789) plus its split offset and Base64."""
+    index: int
+    offset: int
+    length: int
+    hash: str
+    b64: Optional[bytes] = None
+
+
+@dataclass
+class UploadResult:
+    file_id: str
+    fragments: List[Fragment]
+
+
+class FragmentEngine:
+    """One dfs_ctx on one gfx950 device."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = ctypes.c_void_p()
+        check(lib().dfs_open(ctypes.byref(self._ctx), device), "dfs_open")
+        self.device = device
+
+    # -- context -------------------------------------------------------------
+    def close(self) -> None:
+        if self._ctx:
+            lib().dfs_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self) -> ctypes.c_void_p:
+        return self._ctx
+
+    def set_stream(self, stream_handle: int) -> None:
+        check(lib().dfs_set_stream(self._ctx, ctypes.c_void_p(stream_handle or None)), "dfs_set_stream")
+
+    def set_profiling(self, on: bool) -> None:
+        check(lib().dfs_set_profiling(self._ctx, int(on)), "dfs_set_profiling")
+
+    def timings(self) -> dict:
+        ms = (ctypes.c_float * L.DFS_T_COUNT)()
+        check(lib().dfs_get_timings(self._ctx, ms, L.DFS_T_COUNT), "dfs_get_timings")
+        names = ["sha", "b64enc", "b64dec", "gather", "total"]
+        return {k: (v if v >= 0 else None) for k, v in zip(names, ms)}
+
+    # -- sha256Hex (SN:603-613) ----------------------------------------------
+    def sha256(self, messages: Sequence[bytes]) -> List[bytes]:
+        buf, spans = _pack(messages)
+        n = len(messages)
+        out = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        check(lib().dfs_sha256_batch(self._ctx, _ptr(buf), _ptr(spans), n, _ptr(out), 0), "dfs_sha256_batch")
+        return [out[i].tobytes() for i in range(n)]
+
+    def sha256_spans(self, buf: np.ndarray, spans: np.ndarray) -> np.ndarray:
+        n = len(spans)
+        out = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        spans = np.ascontiguousarray(spans, dtype=np.uint64)
+        check(lib().dfs_sha256_batch(self._ctx, _ptr(buf), _ptr(spans), n, _ptr(out), 0), "dfs_sha256_batch")
+        return out[:n]
+
+    def sha256_hex(self, data: bytes) -> str:
+        return self.sha256([data])[0].hex()
+
+    # -- Base64 (SN:636 encode, SN:281 decode) --------------------------------
+    def b64_encode(self, messages: Sequence[bytes]) -> List[bytes]:
+        buf, spans = _pack(messages)
+        n = len(messages)
+        total = sum(b64_encoded_len(len(m)) for m in messages)
+        out = np.zeros(max(total, 1), dtype=np.uint8)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        check(lib().dfs_b64_encode_batch(self._ctx, _ptr(buf), _ptr(spans), n, _ptr(out), total, _ptr(off), 0),
+              "dfs_b64_encode_batch")
+        return [out[int(off[i]):int(off[i + 1])].tobytes() for i in range(n)]
+
+    def b64_decode(self, texts: Sequence[bytes], out_offsets: Optional[Sequence[int]] = None
+                   ) -> List[Optional[bytes]]:
+        """Decoded bytes per message, None where the JDK would throw."""
+        buf, spans = _pack(texts)
+        n = len(texts)
+        caps = [lib().dfs_b64_decoded_cap(len(t)) for t in texts]
+        if out_offsets is None:
+            out_off = np.zeros(max(n, 1), dtype=np.uint64)
+            o = 0
+            for i, c in enumerate(caps):
+                out_off[i] = o
+                o += c
+        else:
+            out_off = np.array(list(out_offsets) + [0] * (n == 0), dtype=np.uint64)
+        end = max([int(out_off[i]) + caps[i] for i in range(n)] + [1])
+        out = np.zeros(end, dtype=np.uint8)
+        out_len = np.zeros(max(n, 1), dtype=np.uint64)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        rc = lib().dfs_b64_decode_batch(self._ctx, _ptr(buf), _ptr(spans), n, _ptr(out), _ptr(out_off),
+                                       _ptr(out_len), _ptr(status), 0)
+        if rc not in (L.DFS_OK, L.DFS_E_DECODE):
+            check(rc, "dfs_b64_decode_batch")
+        res: List[Optional[bytes]] = []
+        for i in range(n):
+            if status[i] != 0:
+                res.append(None)
+            else:
+                o = int(out_off[i])
+                res.append(out[o:o + int(out_len[i])].tobytes())
+        return res
+
+    def b64_decode_one(self, text: bytes) -> bytes:
+        r = self.b64_decode([text])[0]
+        if r is None:
+            raise IllegalArgumentException("Illegal base64 input")
+        return r
+
+    # -- handleUpload (SN:118-189) ---------------------------------------------
+    def upload(self, files: Sequence[bytes], nfrag: int, with_b64: bool = True) -> List[UploadResult]:
+        buf, spans = _pack(files)
+        nf = len(files)
+        fd = np.zeros((max(nf, 1), 32), dtype=np.uint8)
+        frd = np.zeros((max(nf * nfrag, 1), 32), dtype=np.uint8)
+        b64_off = np.zeros(nf * nfrag + 1, dtype=np.uint64)
+        total = sum(b64_encoded_len(ln) for f in files for (_, ln) in split_plan(len(f), nfrag))
+        b64 = np.zeros(max(total, 1), dtype=np.uint8)
+        flags = 0 if with_b64 else L.DFS_NO_B64
+        check(lib().dfs_upload_batch(self._ctx, _ptr(buf), _ptr(spans), nf, nfrag, _ptr(fd), _ptr(frd),
+                                     _ptr(b64), total, _ptr(b64_off), flags), "dfs_upload_batch")
+        out = []
+        for f in range(nf):
+            frags = []
+            for i, (off, ln) in enumerate(split_plan(len(files[f]), nfrag)):
+                k = f * nfrag + i
+                data = b64[int(b64_off[k]):int(b64_off[k + 1])].tobytes() if with_b64 else None
+                frags.append(Fragment(i, off, ln, frd[k].tobytes().hex(), data))
+            out.append(UploadResult(fd[f].tobytes().hex(), frags))
+        return out
+
+    # -- handleDownload gather + verify (SN:419-458) ------------------------------
+    def reassemble_verify(self, frags: Sequence[Sequence[Optional[bytes]]],
+                          expected_file_ids: Optional[Sequence[str]] = None
+                          ) -> List[Tuple[int, Optional[bytes], str]]:
+        """Per file: (status, rebuilt bytes or None, sha256 hex of rebuilt bytes)."""
+        nfiles = len(frags)
+        nfrag = len(frags[0]) if nfiles else 1
+        keep = []
+        ptrs = (ctypes.c_void_p * max(nfiles * nfrag, 1))()
+        lens = np.zeros(max(nfiles * nfrag, 1), dtype=np.uint64)
+        file_off = np.zeros(max(nfiles, 1), dtype=np.uint64)
+        o = 0
+        for f in range(nfiles):
+            file_off[f] = o
+            for i in range(nfrag):
+                d = frags[f][i]
+                k = f * nfrag + i
+                if d is None:
+                    ptrs[k] = None
+                    lens[k] = 1  # a missing fragment: SN:443-446
+                else:
+                    a = np.frombuffer(d, dtype=np.uint8).copy() if d else np.zeros(1, np.uint8)
+                    keep.append(a)
+                    ptrs[k] = a.ctypes.data
+                    lens[k] = len(d)
+            o += int(sum(lens[f * nfrag:(f + 1) * nfrag]))
+        out = np.zeros(max(o, 1), dtype=np.uint8)
+        exp = None
+        if expected_file_ids is not None:
+            exp = np.frombuffer(b"".join(bytes.fromhex(h) for h in expected_file_ids), dtype=np.uint8).copy()
+        dig = np.zeros((max(nfiles, 1), 32), dtype=np.uint8)
+        status = np.zeros(max(nfiles, 1), dtype=np.int32)
+        rc = lib().dfs_reassemble_verify(self._ctx, ptrs, _ptr(lens), nfiles, nfrag, _ptr(out), _ptr(file_off),
+                                        _ptr(exp) if exp is not None else None, _ptr(dig), _ptr(status), 0)
+        if rc not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_CORRUPT):
+            check(rc, "dfs_reassemble_verify")
+        res = []
+        for f in range(nfiles):
+            st = int(status[f])
+            ln = int(sum(lens[f * nfrag:(f + 1) * nfrag]))
+            body = None if st == L.DFS_E_MISSING else out[int(file_off[f]):int(file_off[f]) + ln].tobytes()
+            res.append((st, body, dig[f].tobytes().hex()))
+        return res
+
+    def download(self, b64_frags: Sequence[Sequence[Optional[bytes]]], file_lens: Sequence[int],
+                 frag_hashes: Optional[Sequence[Sequence[str]]] = None,
+                 file_ids: Optional[Sequence[str]] = None) -> List[Tuple[int, Optional[bytes]]]:
+        """Base64 download path: decode into place, per-fragment verify, fileId verify."""
+        nfiles = len(b64_frags)
+        nfrag = len(b64_frags[0]) if nfiles else 1
+        texts, spans = [], np.zeros((max(nfiles * nfrag, 1), 2), dtype=np.uint64)
+        o = 0
+        for f in range(nfiles):
+            for i in range(nfrag):
+                t = b64_frags[f][i]
+                k = f * nfrag + i
+                if t is None:
+                    spans[k] = (0, L.DFS_SPAN_MISSING)
+                else:
+                    spans[k] = (o, len(t))
+                    texts.append(t)
+                    o += len(t)
+        buf = np.frombuffer(b"".join(texts) or b"\0", dtype=np.uint8).copy()
+        flen = np.array(list(file_lens) or [0], dtype=np.uint64)
+        file_off = np.zeros(max(nfiles, 1), dtype=np.uint64)
+        if nfiles > 1:
+            file_off[1:nfiles] = np.cumsum(flen[:nfiles])[:-1]
+        out = np.zeros(max(int(flen[:nfiles].sum()), 1), dtype=np.uint8)
+        ef = None
+        if frag_hashes is not None:
+            ef = np.frombuffer(b"".join(bytes.fromhex(h) for fh in frag_hashes for h in fh), dtype=np.uint8).copy()
+        ei = None
+        if file_ids is not None:
+            ei = np.frombuffer(b"".join(bytes.fromhex(h) for h in file_ids), dtype=np.uint8).copy()
+        status = np.zeros(max(nfiles, 1), dtype=np.int32)
+        rc = lib().dfs_download_batch(self._ctx, _ptr(buf), _ptr(spans), nfiles, nfrag, _ptr(flen),
+                                     _ptr(ef) if ef is not None else None, _ptr(ei) if ei is not None else None,
+                                     _ptr(out), _ptr(file_off), _ptr(status), 0)
+        if rc not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_DECODE, L.DFS_E_FRAG_MISMATCH, L.DFS_E_CORRUPT):
+            check(rc, "dfs_download_batch")
+        res = []
+        for f in range(nfiles):
+            st = int(status[f])
+            o = int(file_off[f])
+            res.append((st, out[o:o + int(flen[f])].tobytes() if st == 0 else None))
+        return res
+
+
+class UploadPlan:
+    """dfs_upload_plan over device-resident (torch) buffers — the bench path."""
+
+    def __init__(self, engine: FragmentEngine, spans: np.ndarray, nfrag: int):
+        self.engine = engine
+        spans = np.ascontiguousarray(spans, dtype=np.uint64)
+        self.nfiles = len(spans)
+        self.nfrag = nfrag
+        self._plan = ctypes.c_void_p()
+        total = ctypes.c_uint64(0)
+        check(lib().dfs_upload_plan_create(engine.ctx, _ptr(spans), self.nfiles, nfrag, ctypes.byref(self._plan),
+                                           ctypes.byref(total)), "dfs_upload_plan_create")
+        self.b64_total = total.value
+
+    def b64_offsets(self) -> np.ndarray:
+        off = np.zeros(self.nfiles * self.nfrag + 1, dtype=np.uint64)
+        check(lib().dfs_upload_plan_b64_offsets(self._plan, _ptr(off)), "dfs_upload_plan_b64_offsets")
+        return off
+
+    def run(self, d_files: int, d_file_digest: int, d_frag_digest: int, d_b64: int, flags: int = 0) -> None:
+        check(lib().dfs_upload_plan_run(self.engine.ctx, self._plan, ctypes.c_void_p(d_files),
+                                        ctypes.c_void_p(d_file_digest or None), ctypes.c_void_p(d_frag_digest),
+                                        ctypes.c_void_p(d_b64 or None), flags), "dfs_upload_plan_run")
+
+    def close(self) -> None:
+        if self._plan:
+            lib().dfs_upload_plan_destroy(self._plan)
+            self._plan = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def synth_fill(engine: FragmentEngine, d_dst: int, spans: np.ndarray, first_file: int, seed: int) -> None:
+    spans = np.ascontiguousarray(spans, dtype=np.uint64)
+    check(lib().dfs_synth_fill(engine.ctx, ctypes.c_void_p(d_dst), _ptr(spans), len(spans), first_file, seed),
+          "dfs_synth_fill")

@@ -1,0 +1,178 @@
+/*
+ * dfs_gpu.h — C ABI of libdfsgpu.so, the MI355X (gfx950) fragment pipeline.
+ *
+ * This is the drop-in boundary for StorageNode's fragment pipeline
+ * (hiagoluansilva/distributed-file-storage, storage-node/src/StorageNode.java,
+ * cited as SN:line).  The reference has no plugin/FFI API: its hot path is
+ * private methods and JDK calls.  Each entry point below replaces the listed
+ * reference sites; a Java host binds them through FFM (java.lang.foreign) or
+ * JNI as shown in INTEGRATION.md.  HTTP routes, JSON bodies, manifest.json and
+ * the on-disk layout are unchanged.
+ *
+ * Conventions
+ *  - Plain C types only.  The caller owns every buffer; the library never
+ *    returns memory.  The library owns device scratch and streams in a ctx.
+ *  - Every function returns an int: DFS_OK (0) or a negative DFS_E_* code.
+ *  - Data pointers are host memory unless `flags` has DFS_DEVICE_PTRS, in
+ *    which case they are HIP device pointers and the call is asynchronous on
+ *    the ctx's stream (see dfs_set_stream); descriptor arrays (spans, offsets,
+ *    pointer tables) are always host memory.
+ *  - Digests are the raw 32-byte SHA-256; the Java side formats lowercase hex
+ *    exactly as sha256Hex does (SN:607-609).
+ *  - A ctx serialises its own calls (one mutex), so StorageNode's
+ *    thread-per-connection handlers (SN:30) may share one ctx.
+ *  - No CPU fallback: without a usable gfx950 device dfs_open fails with
+ *    DFS_E_NODEV and nothing else runs.
+ */
+#ifndef DFS_GPU_H
+#define DFS_GPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFS_ABI_VERSION 1
+
+/* Return codes. */
+#define DFS_OK 0
+#define DFS_E_ARG (-1)          /* invalid argument / capacity too small          */
+#define DFS_E_HIP (-2)          /* HIP runtime error (maps to RuntimeException,   */
+                                /* the catch-all of sha256Hex, SN:610-611)        */
+#define DFS_E_NOMEM (-3)        /* device or pinned allocation failed             */
+#define DFS_E_DECODE (-4)       /* Base64 IllegalArgumentException (SN:281)       */
+#define DFS_E_MISSING (-5)      /* "Could not retrieve fragment i" (SN:443-446)   */
+#define DFS_E_CORRUPT (-6)      /* "File corrupted": SHA-256(file)!=fileId (SN:455)*/
+#define DFS_E_FRAG_MISMATCH (-7) /* "Hash mismatch on fragment" (SN:250-257)      */
+#define DFS_E_NODEV (-8)        /* no gfx950 device                               */
+
+/* Flags. */
+#define DFS_DEVICE_PTRS 0x1u    /* data pointers are device pointers; async       */
+#define DFS_NO_FILEID 0x2u      /* upload: skip the whole-file SHA-256            */
+#define DFS_NO_B64 0x4u         /* upload: skip the Base64 encode                 */
+#define DFS_SERIAL 0x8u         /* upload: run SHA and Base64 on one stream       */
+
+typedef struct dfs_ctx dfs_ctx;
+typedef struct dfs_upload_plan dfs_upload_plan;
+
+/* One message: `len` bytes starting `off` bytes past a base pointer. */
+typedef struct dfs_span {
+    uint64_t off;
+    uint64_t len;
+} dfs_span;
+#define DFS_SPAN_MISSING UINT64_MAX
+
+/* ---- context ------------------------------------------------------------ */
+int dfs_open(dfs_ctx** ctx, int device);
+int dfs_close(dfs_ctx* ctx);
+const char* dfs_strerror(int code);
+int dfs_abi_version(void);
+/* Run subsequent calls on `hip_stream` (a hipStream_t; NULL = the ctx's own). */
+int dfs_set_stream(dfs_ctx* ctx, void* hip_stream);
+/* When on, every call records HIP events around each kernel on the stream it
+ * is launched on; dfs_get_timings returns the last call's per-stage ms. */
+int dfs_set_profiling(dfs_ctx* ctx, int on);
+#define DFS_T_SHA 0      /* multi-message SHA-256 kernel          */
+#define DFS_T_B64ENC 1   /* Base64 encode kernel                  */
+#define DFS_T_B64DEC 2   /* Base64 decode (+ fused gather) kernel */
+#define DFS_T_GATHER 3   /* reassembly gather kernel              */
+#define DFS_T_TOTAL 4    /* whole call, first launch to last     */
+#define DFS_T_COUNT 5
+int dfs_get_timings(dfs_ctx* ctx, float* ms, int n);
+
+/* ---- pure host helpers (no device) ---------------------------------------- */
+/* handleUpload's split (SN:138-171): fragment i has floor(S/N) + (i < S mod N)
+ * bytes, contiguous, in order.  frags: nfrag entries. */
+int dfs_split_plan(uint64_t file_len, uint32_t nfrag, dfs_span* frags);
+/* 4*ceil(n/3): length of Base64.getEncoder().encodeToString (SN:636). */
+uint64_t dfs_b64_encoded_len(uint64_t n);
+/* 3*ceil(n/4): capacity bound for decoding n Base64 chars (SN:281). */
+uint64_t dfs_b64_decoded_cap(uint64_t n);
+/* Placement (SN:143-145, 196-205, 427-428): the 0-based nodes holding
+ * fragment f are holders[0] = f and holders[1] = (f-1+N) mod N; node k
+ * stores {k, (k+1) mod N}. */
+int dfs_fragment_holders(uint32_t frag, uint32_t nfrag, uint32_t holders[2]);
+
+/* ---- batch entry points ----------------------------------------------------- */
+/* sha256Hex at SN:127, 159, 282, 454 for `n` messages of one buffer:
+ * digests[32*i] = SHA-256(base + msgs[i].off, msgs[i].len). */
+int dfs_sha256_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* msgs, uint32_t n,
+                     uint8_t* digests, uint32_t flags);
+
+/* Base64.getEncoder().encodeToString at SN:636 for `n` messages.  Output i is
+ * written at out + out_off[i]; out_off (n+1 entries) is computed by the
+ * library as the prefix sum of dfs_b64_encoded_len and returned. */
+int dfs_b64_encode_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* msgs, uint32_t n,
+                         char* out, uint64_t out_cap, uint64_t* out_off, uint32_t flags);
+
+/* Base64.getDecoder().decode at SN:281 for `n` messages of `in`.  Message i
+ * decodes to out + out_off[i] (caller layout, capacity dfs_b64_decoded_cap);
+ * out_len[i] = bytes written; status[i] = 0 or DFS_E_DECODE where the JDK
+ * throws IllegalArgumentException.  Returns DFS_E_DECODE if any message
+ * failed (after every message was processed). */
+int dfs_b64_decode_batch(dfs_ctx* ctx, const char* in, const dfs_span* msgs, uint32_t n,
+                         uint8_t* out, const uint64_t* out_off, uint64_t* out_len, int32_t* status,
+                         uint32_t flags);
+
+/* The upload half of handleUpload (SN:118-189) for a batch of files:
+ * fileId (SN:127), N-way split (SN:138-157), fragment SHA-256 (SN:159) and
+ * the Base64 of every fragment (SN:636), encoded once each.
+ *   file_digest: nfiles*32            frag_digest: nfiles*nfrag*32
+ *   b64: concatenation in (file, fragment) order; b64_off: nfiles*nfrag+1
+ *   prefix offsets, computed and returned by the library.
+ * b64 may be NULL with DFS_NO_B64. */
+int dfs_upload_batch(dfs_ctx* ctx, const uint8_t* files, const dfs_span* file_spans, uint32_t nfiles,
+                     uint32_t nfrag, uint8_t* file_digest, uint8_t* frag_digest, char* b64,
+                     uint64_t b64_cap, uint64_t* b64_off, uint32_t flags);
+
+/* handleDownload's gather + verify (SN:419-458): file f is rebuilt at
+ * out + file_off[f] from fragments frag_src[f*nfrag+i] (frag_len bytes each,
+ * in index order, SN:448); file_digest_out[f] = SHA-256(rebuilt file) (SN:454)
+ * and status[f] = 0, DFS_E_MISSING (a NULL source, SN:443-446) or
+ * DFS_E_CORRUPT (digest != expected_file_digest[f], SN:455-458).
+ * expected_file_digest may be NULL (status then only reports MISSING). */
+int dfs_reassemble_verify(dfs_ctx* ctx, const uint8_t* const* frag_src, const uint64_t* frag_len,
+                          uint32_t nfiles, uint32_t nfrag, uint8_t* out, const uint64_t* file_off,
+                          const uint8_t* expected_file_digest, uint8_t* file_digest_out,
+                          int32_t* status, uint32_t flags);
+
+/* Download with Base64 transport: per file, Base64-decode each fragment
+ * (SN:281) straight into its place in the file (gather keyed on the split
+ * offsets, SN:138-157/448), SHA-256 every fragment against the upload-time
+ * digests (the receiver/sender check of SN:282 + 250-257), then SHA-256 the
+ * whole file against its fileId (SN:454-458).
+ *   b64_msgs: nfiles*nfrag spans into `b64`; a span with
+ *             len == DFS_SPAN_MISSING marks a fragment no holder could
+ *             supply -> DFS_E_MISSING
+ *   file_len: original sizes (the split plan is recomputed from them)
+ *   expected_frag_digest: nfiles*nfrag*32 (may be NULL)
+ *   expected_file_digest: nfiles*32 (may be NULL)
+ *   status[f]: 0 / DFS_E_MISSING / DFS_E_DECODE / DFS_E_FRAG_MISMATCH /
+ *              DFS_E_CORRUPT (first failure in pipeline order).
+ * status is host memory in every mode; the call synchronises. */
+int dfs_download_batch(dfs_ctx* ctx, const char* b64, const dfs_span* b64_msgs, uint32_t nfiles,
+                       uint32_t nfrag, const uint64_t* file_len, const uint8_t* expected_frag_digest,
+                       const uint8_t* expected_file_digest, uint8_t* out, const uint64_t* file_off,
+                       int32_t* status, uint32_t flags);
+
+/* ---- prepared upload (descriptor build once, run many; device pointers) --- */
+int dfs_upload_plan_create(dfs_ctx* ctx, const dfs_span* file_spans, uint32_t nfiles, uint32_t nfrag,
+                           dfs_upload_plan** plan, uint64_t* b64_total);
+/* Copy the plan's nfiles*nfrag+1 Base64 offsets to host memory. */
+int dfs_upload_plan_b64_offsets(const dfs_upload_plan* plan, uint64_t* b64_off);
+/* Run the plan on device buffers (always asynchronous on the ctx stream). */
+int dfs_upload_plan_run(dfs_ctx* ctx, dfs_upload_plan* plan, const uint8_t* d_files,
+                        uint8_t* d_file_digest, uint8_t* d_frag_digest, char* d_b64, uint32_t flags);
+int dfs_upload_plan_destroy(dfs_upload_plan* plan);
+
+/* ---- synthetic data (bench / tests) -------------------------------------- */
+/* Byte o of file (first_file_index + f) is byte o mod 8 (little endian) of
+ * splitmix64(seed ^ (file_index << 40 | o >> 3)); written at
+ * d_dst + file_spans[f].off (device pointer). */
+int dfs_synth_fill(dfs_ctx* ctx, uint8_t* d_dst, const dfs_span* file_spans, uint32_t nfiles,
+                   uint64_t first_file_index, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFS_GPU_H */

@@ -1,0 +1,257 @@
+"""HIP path vs the CPU oracle and the golden vectors (needs a gfx950 GPU).
+
+Bar: bit-exact digests and bytes (integer/byte work).  Every call goes through
+the C ABI of libdfsgpu.so; the oracle is only the checker.
+"""
+import base64
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import dfs_amd
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def kat_bytes(inp):
+    if inp["kind"] == "ascii":
+        return inp["text"].encode()
+    return bytes([inp["byte"]]) * inp["count"]
+
+
+def test_sha256_kats(engine, golden):
+    msgs = [kat_bytes(k["input"]) for k in golden["sha256_kat"]]
+    got = engine.sha256(msgs)
+    assert [g.hex() for g in got] == [k["digest"] for k in golden["sha256_kat"]]
+
+
+def test_sha256_every_length_and_alignment(engine):
+    # lengths 0..300 (every padding case) at every start offset mod 4
+    rng = np.random.default_rng(7)
+    buf = rng.integers(0, 256, 4096, dtype=np.uint8)
+    spans = np.array([(a, n) for n in range(0, 301) for a in (0, 1, 2, 3, 517)], dtype=np.uint64)
+    got = engine.sha256_spans(buf, spans)
+    raw = buf.tobytes()
+    for i, (a, n) in enumerate(spans):
+        assert got[i].tobytes() == hashlib.sha256(raw[a:a + n]).digest(), (a, n)
+
+
+def test_sha256_random_messages_vs_oracle(engine):
+    rng = random.Random(11)
+    msgs = [bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 20000))) for _ in range(40)]
+    msgs += [b"", b"a" * 64, b"b" * 55, b"c" * 56]
+    got = engine.sha256(msgs)
+    for m, g in zip(msgs, got):
+        assert g == O.c_sha256(m)
+
+
+def test_b64_encode_rfc_and_edges(engine, golden):
+    vec = golden["b64_rfc4648"]
+    got = engine.b64_encode([v["input"].encode() for v in vec])
+    assert [g.decode() for g in got] == [v["output"] for v in vec]
+    rng = np.random.default_rng(3)
+    raw = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    msgs = [raw[a:a + n] for n in list(range(0, 40)) + [12287, 12288, 12289, 24577, 65536]
+            for a in (0, 1, 2, 3)]
+    got = engine.b64_encode(msgs)
+    for m, g in zip(msgs, got):
+        assert g == base64.b64encode(m)
+        assert g == O.c_b64_encode(m)
+
+
+def test_b64_decode_jdk_cases(engine, golden):
+    cases = golden["b64_decode_jdk"]
+    got = engine.b64_decode([bytes.fromhex(d["input_hex"]) for d in cases])
+    for d, g in zip(cases, got):
+        want = None if d["output_hex"] is None else bytes.fromhex(d["output_hex"])
+        assert g == want, d["input_hex"]
+    with pytest.raises(dfs_amd.IllegalArgumentException):
+        engine.b64_decode_one(b"Zm9v=")
+
+
+def test_b64_decode_alignments_and_lengths(engine):
+    rng = np.random.default_rng(5)
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+             for n in list(range(0, 60)) + [4095, 4096, 12288, 12289, 50001]]
+    texts = [base64.b64encode(d) for d in datas]
+    for pad_in in (0, 1, 2, 3):
+        # misalign inputs by prefixing the packed buffer, and outputs by offsets
+        for out_shift in (0, 1, 2, 3):
+            offs, o = [], out_shift
+            for d in datas:
+                offs.append(o)
+                o += len(d) + 5 + out_shift
+            msgs = [b"x" * pad_in + t for t in texts]
+            # decode the prefixed texts: the prefix makes them invalid, so build spans by hand
+            buf = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+            spans, p = [], 0
+            for t in msgs:
+                spans.append((p + pad_in, len(t) - pad_in))
+                p += len(t)
+            got = _decode_spans(engine, buf, spans, offs)
+            for d, g in zip(datas, got):
+                assert g == d
+
+
+def _decode_spans(engine, buf, spans, out_off):
+    import ctypes
+    n = len(spans)
+    spans = np.array(spans, dtype=np.uint64)
+    caps = [int(dfs_amd.lib().dfs_b64_decoded_cap(int(s[1]))) for s in spans]
+    out_off = np.array(out_off, dtype=np.uint64)
+    out = np.zeros(int(max(out_off + np.array(caps, dtype=np.uint64))) + 1, dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    rc = dfs_amd.lib().dfs_b64_decode_batch(engine.ctx, buf.ctypes.data, spans.ctypes.data, n, out.ctypes.data,
+                                            out_off.ctypes.data, out_len.ctypes.data, status.ctypes.data, 0)
+    assert rc in (0, dfs_amd.DFS_E_DECODE)
+    return [None if status[i] else out[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes()
+            for i in range(n)]
+
+
+def test_b64_decode_fuzz_vs_oracle(engine):
+    rng = random.Random(17)
+    alphabet = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/="
+    texts = []
+    for _ in range(2000):
+        n = rng.randrange(0, 40)
+        texts.append(bytes(rng.choice(alphabet + b"-_ \n\xff") for _ in range(n)))
+    # long valid texts with one corrupted char somewhere
+    for _ in range(40):
+        d = bytes(rng.getrandbits(8) for _ in range(rng.randrange(100, 30000)))
+        t = bytearray(base64.b64encode(d))
+        t[rng.randrange(len(t))] = rng.choice(b"*-_= \n")
+        texts.append(bytes(t))
+    got = engine.b64_decode(texts)
+    for t, g in zip(texts, got):
+        assert g == O.c_b64_decode(t), t[:40]
+
+
+def test_examples_upload_matches_golden(engine, golden, example_bytes):
+    names = [e["name"] for e in golden["examples"]]
+    res = engine.upload([example_bytes[n] for n in names], 5)
+    for e, r in zip(golden["examples"], res):
+        assert r.file_id == e["fileId"]
+        for f, g in zip(e["fragments"], r.fragments):
+            assert (g.index, g.offset, g.length, g.hash) == (f["index"], f["offset"], f["length"], f["sha256"])
+            assert len(g.b64) == f["b64_len"]
+            assert hashlib.sha256(g.b64).hexdigest() == f["b64_sha256"]
+            if "b64" in f:
+                assert g.b64.decode() == f["b64"]
+        # the reference's per-fragment log line (SN:160), uploader node 1
+        lines = ["[1] Fragment %d: %d bytes, hash=%s" % (g.index, g.length, g.hash) for g in r.fragments]
+        assert lines == e["log_lines"]
+
+
+def test_edge_sizes_upload(engine, golden):
+    for nfrag in (5, 8):
+        recs = [e for e in golden["edge"] if e["nfrag"] == nfrag]
+        files = [O.c_synth(e["synth_file_index"], 0, e["size"]) for e in recs]
+        res = engine.upload(files, nfrag)
+        for e, r in zip(recs, res):
+            assert r.file_id == e["fileId"]
+            for f, g in zip(e["fragments"], r.fragments):
+                assert g.hash == f["sha256"]
+                assert hashlib.sha256(g.b64).hexdigest() == f["b64_sha256"]
+
+
+def test_upload_batch_vs_oracle_mixed_sizes(engine):
+    rng = random.Random(23)
+    sizes = [rng.choice([0, 1, 4, 63, 64, 65, 999, 4096, 70001, 1 << 18]) for _ in range(60)] + [1 << 20] * 4
+    files = [O.c_synth(1000 + i, 0, s) for i, s in enumerate(sizes)]
+    for nfrag in (5, 8):
+        res = engine.upload(files, nfrag)
+        fd, frd, b64, off = O.c_upload_batch(files, nfrag, threads=4)
+        for f, r in enumerate(res):
+            assert r.file_id == fd[f].tobytes().hex()
+            for i, g in enumerate(r.fragments):
+                k = f * nfrag + i
+                assert g.hash == frd[f, i].tobytes().hex()
+                assert g.b64 == b64[int(off[k]):int(off[k + 1])]
+
+
+def test_reassemble_verify(engine, example_bytes):
+    files = [example_bytes["id.jpg"], example_bytes["teste.txt"], O.c_synth(9, 0, 100003)]
+    ups = engine.upload(files, 5)
+    frags = [[d[g.offset:g.offset + g.length] for g in u.fragments] for d, u in zip(files, ups)]
+    res = engine.reassemble_verify(frags, [u.file_id for u in ups])
+    for d, (st, body, h) in zip(files, res):
+        assert st == 0 and body == d and h == hashlib.sha256(d).hexdigest()
+    # corrupted fragment -> "File corrupted" (SN:455-458); missing -> SN:443-446
+    bad = [list(f) for f in frags]
+    bad[0][2] = bytes([bad[0][2][0] ^ 1]) + bad[0][2][1:]
+    bad[1][4] = None
+    res = engine.reassemble_verify(bad, [u.file_id for u in ups])
+    assert res[0][0] == dfs_amd.DFS_E_CORRUPT
+    assert res[1][0] == dfs_amd.DFS_E_MISSING
+    assert res[2][0] == 0
+
+
+def test_download_base64_path(engine, example_bytes):
+    files = [example_bytes[n] for n in ("id.jpg", "pl.png", "pag1.html", "teste.txt")] + \
+        [O.c_synth(77, 0, 262144), O.c_synth(78, 0, 3), b""]
+    for nfrag in (5, 8):
+        ups = engine.upload(files, nfrag)
+        b64 = [[g.b64 for g in u.fragments] for u in ups]
+        hashes = [[g.hash for g in u.fragments] for u in ups]
+        ids = [u.file_id for u in ups]
+        res = engine.download(b64, [len(f) for f in files], hashes, ids)
+        for d, (st, body) in zip(files, res):
+            assert st == 0 and body == d
+        # failure modes, first failure in pipeline order
+        b2 = [list(x) for x in b64]
+        b2[0][1] = None                                   # missing
+        b2[1][0] = b2[1][0][:-1] + b"*"                    # IllegalArgumentException
+        h2 = [list(x) for x in hashes]
+        h2[2][3] = "00" * 32                               # per-fragment mismatch
+        i2 = list(ids)
+        i2[3] = "11" * 32                                  # fileId mismatch
+        res = engine.download(b2, [len(f) for f in files], h2, i2)
+        assert [r[0] for r in res[:4]] == [dfs_amd.DFS_E_MISSING, dfs_amd.DFS_E_DECODE,
+                                           dfs_amd.DFS_E_FRAG_MISMATCH, dfs_amd.DFS_E_CORRUPT]
+        assert all(r[0] == 0 for r in res[4:])
+
+
+def test_device_plan_and_synth_vs_oracle(engine):
+    import torch
+    nfiles, S, nfrag = 96, (1 << 16) + 5, 5
+    spans = np.array([(f * S, S) for f in range(nfiles)], dtype=np.uint64)
+    files = torch.empty(nfiles * S + 16, dtype=torch.uint8, device="cuda")
+    dfs_amd.synth_fill(engine, files.data_ptr(), spans, 0, O.SYNTH_SEED)
+    torch.cuda.synchronize()
+    host = files.cpu().numpy()
+    for f in (0, 1, 95):
+        assert host[f * S:(f + 1) * S].tobytes() == O.c_synth(f, 0, S)
+    plan = dfs_amd.UploadPlan(engine, spans, nfrag)
+    fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
+    frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
+    b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+    engine.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        for flags in (0, dfs_amd.DFS_SERIAL):
+            fd.zero_(); frd.zero_(); b64.zero_()
+            plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), flags)
+            torch.cuda.synchronize()
+            files_b = [host[f * S:(f + 1) * S].tobytes() for f in range(nfiles)]
+            efd, efrd, eb64, eoff = O.c_upload_batch(files_b, nfrag, threads=8)
+            assert (fd.cpu().numpy().reshape(nfiles, 32) == efd).all()
+            assert (frd.cpu().numpy().reshape(nfiles, nfrag, 32) == efrd).all()
+            assert b64.cpu().numpy().tobytes() == eb64
+            assert (plan.b64_offsets() == eoff).all()
+    finally:
+        engine.set_stream(0)
+        plan.close()
+
+
+def test_profiling_timings(engine):
+    engine.set_profiling(True)
+    try:
+        engine.upload([O.c_synth(3, 0, 1 << 20)] * 8, 5)
+        t = engine.timings()
+        assert t["sha"] is not None and t["sha"] > 0
+        assert t["b64enc"] is not None and t["b64enc"] > 0
+    finally:
+        engine.set_profiling(False)
