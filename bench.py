@@ -85,7 +85,7 @@ def cpu_baseline(args, log):
         secs, _, _ = O.cpu_upload_bench(2 * threads, S, N, threads, use_openssl=False)
         kind_sha = "scalar"
     per_file = max(secs, 1e-6) / 2.0  # seconds per file per thread
-    nfiles = int(max(threads, min(20000, args.cpu_seconds / per_file * threads)))
+    nfiles = int(max(threads, min(200000, args.cpu_seconds / per_file * threads)))
     secs, _, _ = O.cpu_upload_bench(nfiles, S, N, threads, use_openssl=(kind_sha == "openssl"))
     gbs = nfiles * S / secs / 1e9
     log(f"cpu baseline: {nfiles} files x {S} B on {threads} threads: {secs:.2f} s -> {gbs:.3f} GB/s")
@@ -177,7 +177,7 @@ def main():
         log(f"oracle spot-check of {len(idx)} files: {'OK' if ok else 'MISMATCH'}")
 
     # ---- numbers -----------------------------------------------------------------
-    total_bytes = F * S * world
+    total_bytes = F * S * world * args.steps  # file bytes all ranks pushed through the timed steps
     value = total_bytes / elapsed / 1e9
     lens = split(S, N)
     blocks = F * (sha_blocks(S) + sum(sha_blocks(x) for x in lens))

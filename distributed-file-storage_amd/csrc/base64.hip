@@ -38,6 +38,9 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
                                                                   char* __restrict__ out) {
+    // Memory-bound waves issue first: beside the VALU-bound SHA kernel they
+    // need few issue slots but must keep their loads in flight.
+    __builtin_amdgcn_s_setprio(3);
     __shared__ uint32_t lut_words[16];
     if (threadIdx.x < 16) lut_words[threadIdx.x] = kAlphaWords[threadIdx.x];
     __syncthreads();
@@ -56,20 +59,28 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
         uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(out) + jobs[j].dst_off;
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
         const uint64_t g0 = (t - jobs[j].tile_start) * kEncGroupsPerTile + threadIdx.x;
+        constexpr int kPer = kEncGroupsPerTile / kStreamBlock;
+        // Issue every group's loads first (memory-level parallelism), then
+        // encode and store.
+        uint4 raw[kPer];
 #pragma unroll
-        for (int i = 0; i < kEncGroupsPerTile / kStreamBlock; ++i) {
+        for (int i = 0; i < kPer; ++i) {
             const uint64_t g = g0 + static_cast<uint64_t>(i) * kStreamBlock;
+            raw[i] = make_uint4(0u, 0u, 0u, 0u);
             if (g < nfg) {
                 const uint32_t* w = reinterpret_cast<const uint32_t*>(src + 12 * g - sa);
-                uint32_t u0, u1, u2;
-                if (sa) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(w);
-                    u0 = align_bytes(v.y, v.x, sa);
-                    u1 = align_bytes(v.z, v.y, sa);
-                    u2 = align_bytes(v.w, v.z, sa);
-                } else {
-                    u0 = w[0]; u1 = w[1]; u2 = w[2];
-                }
+                if (sa) raw[i] = *reinterpret_cast<const uint4*>(w);
+                else raw[i] = make_uint4(w[0], w[1], w[2], 0u);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const uint64_t g = g0 + static_cast<uint64_t>(i) * kStreamBlock;
+            if (g < nfg) {
+                const uint4 v = raw[i];
+                const uint32_t u0 = align_bytes(v.y, v.x, sa);
+                const uint32_t u1 = align_bytes(v.z, v.y, sa);
+                const uint32_t u2 = align_bytes(v.w, v.z, sa);
                 // Big-endian 24-bit groups: bytes (0,1,2) (3,4,5) (6,7,8) (9,10,11).
                 const uint32_t g0v = __builtin_amdgcn_perm(0u, u0, 0x0c000102u);
                 const uint32_t g1v = __builtin_amdgcn_perm(u1, u0, 0x0c030405u);

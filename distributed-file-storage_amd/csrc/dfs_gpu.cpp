@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -50,7 +51,7 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_EXPECT, B_COUNT };
+enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_QUEUE, B_COUNT };
 
 }  // namespace
 
@@ -60,6 +61,7 @@ struct dfs_ctx {
     hipStream_t aux = nullptr;   // second stream (Base64 beside SHA)
     hipStream_t user = nullptr;  // borrowed (dfs_set_stream)
     bool profiling = false;
+    int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
     DevBuf buf[B_COUNT];
@@ -69,6 +71,7 @@ struct dfs_ctx {
 
 struct dfs_upload_plan {
     int device = 0;
+    uint32_t* d_queue = nullptr;  // SHA work-queue word
     uint32_t nfiles = 0, nfrag = 0;
     uint32_t n_all = 0, n_frag_only = 0;  // SHA lanes with / without fileIds
     uint32_t prio_all = 0, prio_frag = 0;
@@ -211,6 +214,7 @@ int dfs_open(dfs_ctx** out, int device) {
     dfs_ctx* c = new (std::nothrow) dfs_ctx;
     if (!c) return DFS_E_NOMEM;
     c->device = device;
+    if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = std::max(1, std::min(8, std::atoi(w)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
@@ -314,7 +318,9 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
     if (int rc = put(c, B_DESC, d.data(), d.size() * sizeof(ShaDesc), s)) return rc;
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_SHA, s);
-    HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig, nullptr, s));
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -500,7 +506,8 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     p->n_frag_only = static_cast<uint32_t>(frag.size());
     p->n_enc = static_cast<uint32_t>(enc.size());
     p->enc_tiles = finish_jobs(enc, items, dfs::kEncGroupsPerTile);
-    hipError_t e = hipMalloc(&p->d_all, std::max<size_t>(all.size(), 1) * sizeof(ShaDesc));
+    hipError_t e = hipMalloc(&p->d_queue, dfs::kShaQueueBytes);
+    if (e == hipSuccess) e = hipMalloc(&p->d_all, std::max<size_t>(all.size(), 1) * sizeof(ShaDesc));
     if (e == hipSuccess) e = hipMalloc(&p->d_frag, std::max<size_t>(frag.size(), 1) * sizeof(ShaDesc));
     if (e == hipSuccess) e = hipMalloc(&p->d_enc, enc.size() * sizeof(StreamJob));
     if (e == hipSuccess && !all.empty())
@@ -527,6 +534,7 @@ int dfs_upload_plan_b64_offsets(const dfs_upload_plan* p, uint64_t* b64_off) {
 int dfs_upload_plan_destroy(dfs_upload_plan* p) {
     if (!p) return DFS_E_ARG;
     (void)hipSetDevice(p->device);
+    if (p->d_queue) (void)hipFree(p->d_queue);
     if (p->d_all) (void)hipFree(p->d_all);
     if (p->d_frag) (void)hipFree(p->d_frag);
     if (p->d_enc) (void)hipFree(p->d_enc);
@@ -545,6 +553,16 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     hipStream_t s = c->stream();
     hipStream_t sb = serial ? s : c->aux;
     Timer tm(c);
+    // Experiment hook: DFS_SHA_CENSUS=<path> dumps {hw_id, xcc_id, t0, t1} per
+    // SHA work item (s_memrealtime, 100 MHz) after the call.
+    const char* census_path = std::getenv("DFS_SHA_CENSUS");
+    uint32_t* census = nullptr;
+    const uint32_t n_items = ((do_fileid ? p->n_all : p->n_frag_only) + 63u) / 64u;
+    if (census_path) {
+        HIPC(c->buf[B_OUTLEN].ensure(16ull * n_items));
+        census = c->buf[B_OUTLEN].as<uint32_t>();
+        HIPC(hipMemsetAsync(census, 0, 16ull * n_items, s));
+    }
     tm.begin(DFS_T_TOTAL, s);
     if (do_b64 && !serial) {  // fork: Base64 on the aux stream beside SHA
         HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER], s));
@@ -553,10 +571,11 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     tm.begin(DFS_T_SHA, s);
     if (do_fileid) {
         // out index < nfiles -> file digest, else fragment digest (split = nfiles)
-        HIPC(dfs::launch_sha256(d_files, p->d_all, p->n_all, p->nfiles, p->prio_all, d_fd, d_frd, nullptr, s));
+        HIPC(dfs::launch_sha256(d_files, p->d_all, p->n_all, p->nfiles, p->prio_all, d_fd, d_frd, p->d_queue,
+                                c->sha_wps, census, s));
     } else {
-        HIPC(dfs::launch_sha256(d_files, p->d_frag, p->n_frag_only, p->nfiles, p->prio_frag, d_fd, d_frd, nullptr,
-                                s));
+        HIPC(dfs::launch_sha256(d_files, p->d_frag, p->n_frag_only, p->nfiles, p->prio_frag, d_fd, d_frd,
+                                p->d_queue, c->sha_wps, census, s));
     }
     tm.end(DFS_T_SHA, s);
     if (do_b64) {
@@ -569,6 +588,15 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
         }
     }
     tm.end(DFS_T_TOTAL, s);
+    if (census_path) {
+        std::vector<uint32_t> h(4ull * n_items);
+        HIPC(hipMemcpyAsync(h.data(), census, h.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        if (FILE* fp = std::fopen(census_path, "wb")) {
+            std::fwrite(h.data(), 4, h.size(), fp);
+            std::fclose(fp);
+        }
+    }
     return DFS_OK;
 }
 }  // namespace
@@ -704,8 +732,9 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     HIPC(dfs::launch_gather(c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s));
     tm.end(DFS_T_GATHER, s);
     tm.begin(DFS_T_SHA, s);
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
-                            d_dig, d_dig, nullptr, s));
+                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<uint8_t> dig(32ull * nfiles);
@@ -791,8 +820,10 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
                                 c->buf[B_STATUS].as<int32_t>(), nullptr, s));
     tm.end(DFS_T_B64DEC, s);
     tm.begin(DFS_T_SHA, s);
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
-                            static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig, nullptr, s));
+                            static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(),
+                            c->sha_wps, nullptr, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(nf);

@@ -30,6 +30,7 @@ struct StreamJob {
 };
 
 constexpr int kShaBlock = 256;       // threads per SHA workgroup (4 waves)
+constexpr size_t kShaQueueBytes = 4 * (64 + 8192);  // SHA queue words + per-SIMD tokens
 constexpr int kStreamBlock = 256;    // threads per stream workgroup
 constexpr int kEncGroupsPerTile = 1024;  // 12-byte groups (4 per thread)
 constexpr int kDecChunksPerTile = 1024;  // 12-byte output chunks (4 per thread)
@@ -42,9 +43,12 @@ inline uint64_t enc_tiles(uint64_t len) {
 }
 
 // Launchers (return hipError_t of the launch).
+// Persistent multi-message SHA-256.  `queue` is kShaQueueBytes of device
+// memory, zeroed by the launcher on `s` before the launch; the grid holds waves_per_simd waves
+// on each of the 1024 SIMDs (fewer for small batches).
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
-                         uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* census,
-                         hipStream_t s);
+                         uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
+                         int waves_per_simd, uint32_t* census, hipStream_t s);
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
                              char* out, hipStream_t s);
 // Decode: chars of job j at in + src_off decode to out + dst_off.

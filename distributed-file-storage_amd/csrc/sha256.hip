@@ -103,93 +103,144 @@ __device__ __forceinline__ uint32_t xcc_id() {
     return v;
 }
 
+// 13-bit id of the SIMD this wave runs on: XCC, SE, SH, CU, SIMD fields of
+// HW_REG_XCC_ID / HW_REG_HW_ID (gfx9 layout).  Used only to balance work
+// (speed), never for correctness.
+__device__ __forceinline__ uint32_t simd_key() {
+    const uint32_t hw = hw_id();
+    return ((xcc_id() & 7u) << 10) | (((hw >> 13) & 7u) << 7) | (((hw >> 12) & 1u) << 6) |
+           (((hw >> 8) & 15u) << 2) | ((hw >> 4) & 3u);
+}
+
+// Persistent: each wave pulls 64-message items (item i = sorted lanes
+// [64i, 64i+64)) from two atomic queues.  Items [0, n_long) carry the long
+// chains (fileIds): a wave may take one only while its SIMD holds fewer than
+// `cap` of them (per-SIMD token counters), so every SIMD runs one long chain
+// at full single-wave issue rate and the short items (fragments) fill the
+// remaining issue slots dynamically.  The grid holds a fixed number of waves
+// per SIMD, leaving the other wave slots to the Base64 kernel beside it.
+// queue[0] = long counter, queue[1] = short counter, queue[64 + key] = SIMD
+// token counters; all zeroed by the launcher before each launch.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restrict__ base,
                                                           const ShaDesc* __restrict__ descs, uint32_t n,
-                                                          uint32_t split, uint32_t prio_lanes,
+                                                          uint32_t split, uint32_t n_long, uint32_t cap,
                                                           uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
+                                                          uint32_t* __restrict__ queue,
                                                           uint32_t* __restrict__ census) {
-    const uint32_t gid = blockIdx.x * kShaBlock + threadIdx.x;
-    const uint32_t wave_first = __builtin_amdgcn_readfirstlane(blockIdx.x * kShaBlock + (threadIdx.x & ~63u));
-    if (wave_first < prio_lanes) __builtin_amdgcn_s_setprio(2);
-    const uint32_t wave_index = wave_first >> 6;
-    uint64_t t_start = 0;
-    if (census) t_start = __builtin_amdgcn_s_memrealtime();
-    if (gid < n) {
-        const ShaDesc d = descs[gid];
-        const uint32_t sh = static_cast<uint32_t>(d.off) & 3u;
-        const uint32_t* __restrict__ p = reinterpret_cast<const uint32_t*>(base + (d.off - sh));
-        const uint32_t sel = (sh + 3u) | ((sh + 2u) << 8) | ((sh + 1u) << 16) | (sh << 24);
-        const uint32_t nfull = static_cast<uint32_t>(d.len >> 6);
-        uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                          0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-        if (nfull) {
-            uint32_t A[16], B[16], xa, xb;
-            load_block(p, sh, A, xa);
-            uint32_t k = 0;
-            for (;;) {
-                // A holds block k; prefetch block k+1 (clamped) into B.
-                load_block(p + 16u * min(k + 1u, nfull - 1u), sh, B, xb);
-                to_be(A, xa, sel);
-                compress(st, A);
-                if (++k >= nfull) break;
-                load_block(p + 16u * min(k + 1u, nfull - 1u), sh, A, xa);
-                to_be(B, xb, sel);
-                compress(st, B);
-                if (++k >= nfull) break;
+    const uint32_t nitems = (n + 63u) >> 6;
+    const uint32_t n_short = nitems - n_long;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t key = simd_key();
+    for (;;) {
+        uint32_t item = 0xffffffffu;
+        if (lane == 0) {
+            if (n_long && __hip_atomic_load(queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n_long &&
+                atomicAdd(queue + 64 + key, 1u) < cap) {
+                const uint32_t it = atomicAdd(queue, 1u);
+                if (it < n_long) item = it;
+            }
+            if (item == 0xffffffffu) {
+                const uint32_t it = atomicAdd(queue + 1, 1u);
+                if (it < n_short) {
+                    item = n_long + it;
+                } else if (n_long) {  // long items a starved SIMD left behind
+                    const uint32_t it2 = atomicAdd(queue, 1u);
+                    if (it2 < n_long) item = it2;
+                }
             }
         }
-        // Tail: r = len mod 64 bytes + FIPS 180-4 §5.1.1 padding, 1 or 2 blocks.
-        const uint32_t r = static_cast<uint32_t>(d.len) & 63u;
-        const uint64_t bits = d.len << 3;
-        const uint32_t ntb = r < 56u ? 1u : 2u;
-        const uint32_t lim = d.len ? sh + r : 0u;  // word i of the tail holds message bytes iff 4i < lim
-        const uint32_t* __restrict__ q = p + 16u * nfull;
-        for (uint32_t tb = 0; tb < ntb; ++tb) {
-            uint32_t T[17], W[16];
+        item = __builtin_amdgcn_readfirstlane(item);
+        if (item == 0xffffffffu) break;
+        if (item < n_long) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+        uint64_t t_start = 0;
+        if (census) t_start = __builtin_amdgcn_s_memrealtime();
+        const uint32_t gid = item * 64u + lane;
+        if (gid < n) {
+            const ShaDesc d = descs[gid];
+            const uint32_t sh = static_cast<uint32_t>(d.off) & 3u;
+            const uint32_t* __restrict__ p = reinterpret_cast<const uint32_t*>(base + (d.off - sh));
+            const uint32_t sel = (sh + 3u) | ((sh + 2u) << 8) | ((sh + 1u) << 16) | (sh << 24);
+            const uint32_t nfull = static_cast<uint32_t>(d.len >> 6);
+            uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                              0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+            if (nfull) {
+                uint32_t A[16], B[16], xa, xb;
+                load_block(p, sh, A, xa);
+                uint32_t k = 0;
+                for (;;) {
+                    // A holds block k; prefetch block k+1 (clamped) into B.
+                    load_block(p + 16u * min(k + 1u, nfull - 1u), sh, B, xb);
+                    to_be(A, xa, sel);
+                    compress(st, A);
+                    if (++k >= nfull) break;
+                    load_block(p + 16u * min(k + 1u, nfull - 1u), sh, A, xa);
+                    to_be(B, xb, sel);
+                    compress(st, B);
+                    if (++k >= nfull) break;
+                }
+            }
+            // Tail: r = len mod 64 bytes + FIPS 180-4 §5.1.1 padding, 1 or 2 blocks.
+            const uint32_t r = static_cast<uint32_t>(d.len) & 63u;
+            const uint64_t bits = d.len << 3;
+            const uint32_t ntb = r < 56u ? 1u : 2u;
+            const uint32_t lim = d.len ? sh + r : 0u;  // word i of the tail holds message bytes iff 4i < lim
+            const uint32_t* __restrict__ q = p + 16u * nfull;
+            for (uint32_t tb = 0; tb < ntb; ++tb) {
+                uint32_t T[17], W[16];
 #pragma unroll
-            for (int i = 0; i < 17; ++i) {
-                const uint32_t wi = 16u * tb + static_cast<uint32_t>(i);
-                T[i] = (4u * wi < lim) ? q[wi] : 0u;
-            }
+                for (int i = 0; i < 17; ++i) {
+                    const uint32_t wi = 16u * tb + static_cast<uint32_t>(i);
+                    T[i] = (4u * wi < lim) ? q[wi] : 0u;
+                }
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const int rem = static_cast<int>(r) - 64 * static_cast<int>(tb) - 4 * j;  // message bytes in word j
-                const uint32_t w = __builtin_amdgcn_perm(T[j + 1], T[j], sel);
-                const uint32_t mask = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
-                const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
-                W[j] = (w & mask) | pad;
+                for (int j = 0; j < 16; ++j) {
+                    const int rem = static_cast<int>(r) - 64 * static_cast<int>(tb) - 4 * j;  // message bytes in word j
+                    const uint32_t w = __builtin_amdgcn_perm(T[j + 1], T[j], sel);
+                    const uint32_t mask = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
+                    const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
+                    W[j] = (w & mask) | pad;
+                }
+                if (tb + 1u == ntb) {
+                    W[14] = static_cast<uint32_t>(bits >> 32);
+                    W[15] = static_cast<uint32_t>(bits);
+                }
+                compress(st, W);
             }
-            if (tb + 1u == ntb) {
-                W[14] = static_cast<uint32_t>(bits >> 32);
-                W[15] = static_cast<uint32_t>(bits);
-            }
-            compress(st, W);
+            uint8_t* dst = d.out < split ? out0 + 32ull * d.out : out1 + 32ull * (d.out - split);
+            uint4* o = reinterpret_cast<uint4*>(dst);
+            o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                              __builtin_bswap32(st[3]));
+            o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                              __builtin_bswap32(st[7]));
         }
-        uint8_t* dst = d.out < split ? out0 + 32ull * d.out : out1 + 32ull * (d.out - split);
-        uint4* o = reinterpret_cast<uint4*>(dst);
-        o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
-                          __builtin_bswap32(st[3]));
-        o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
-                          __builtin_bswap32(st[7]));
-    }
-    if (census && (threadIdx.x & 63u) == 0u) {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        uint32_t* c = census + 4ull * wave_index;
-        c[0] = hw_id();
-        c[1] = xcc_id();
-        c[2] = static_cast<uint32_t>(t_start);
-        c[3] = static_cast<uint32_t>(t_end);
+        if (census && lane == 0u) {
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            uint32_t* c = census + 4ull * item;
+            c[0] = hw_id();
+            c[1] = xcc_id();
+            c[2] = static_cast<uint32_t>(t_start);
+            c[3] = static_cast<uint32_t>(t_end);
+        }
     }
 }
 
 }  // namespace
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
-                         uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s) {
+                         uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
+                         uint32_t* census, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const uint32_t grid = (n + kShaBlock - 1) / kShaBlock;
-    hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, prio_lanes, out0,
-                       out1, census);
+    hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
+    if (e != hipSuccess) return e;
+    const uint32_t n_long = (prio_lanes + 63u) / 64u;
+    const uint32_t cap = (n_long + 1023u) / 1024u;
+    const uint64_t items = (n + 63u) / 64u;
+    uint64_t waves = 1024ull * static_cast<uint64_t>(waves_per_simd < 1 ? 1 : waves_per_simd);
+    if (waves > items) waves = items;
+    const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
+    hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
+                       out1, queue, census);
     return hipGetLastError();
 }
 

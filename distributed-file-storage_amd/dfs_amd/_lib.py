@@ -89,6 +89,15 @@ def lib() -> ctypes.CDLL:
             raise ImportError(
                 f"{LIB_PATH} is not built; run `make -C {PKG_DIR}` (hipcc, gfx950). "
                 "There is no CPU fallback for the fragment pipeline.")
+        # One HIP runtime per process: torch ships its own libamdhip64.so
+        # (soname libamdhip64.so.7, the same soname libdfsgpu.so needs).  If
+        # torch is importable, load it first so libdfsgpu.so binds to the
+        # runtime already in the process instead of pulling in a second copy
+        # from /opt/rocm (two runtimes make torch report "No HIP GPUs").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

@@ -286,10 +286,11 @@ static uint64_t splitmix64(uint64_t x) {
 }
 
 void oracle_synth(uint64_t seed, uint64_t f, uint64_t start, uint64_t len, uint8_t* out) {
-    for (uint64_t i = 0; i < len; i++) {
+    uint64_t i = 0;
+    while (i < len) {
         uint64_t o = start + i;
         uint64_t v = splitmix64(seed ^ ((f << 40) | (o >> 3)));
-        out[i] = (uint8_t)(v >> (8 * (o & 7)));
+        for (uint64_t b = o & 7; b < 8 && i < len; b++, i++) out[i] = (uint8_t)(v >> (8 * b));
     }
 }
 

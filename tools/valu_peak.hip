@@ -1,44 +1,67 @@
-// valu_peak.hip — on-box int32 VALU peak microbenchmark (gfx950).
+// valu_peak.hip — on-box int32 VALU issue-rate microbenchmark (gfx950).
 //
-// Measures sustained wave64 issue rate of the instructions the SHA-256 kernel
-// is made of (v_add3_u32, v_alignbit_b32, v_bitop3_b32, v_add_u32), as
-// 8 independent dependency chains per lane, 8 waves per SIMD, every CU busy.
-// Reported as int32 lane-ops/s; the roofline peak in bench.py is the larger
-// of this and the clock-derived 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
+// For each instruction the SHA-256 / Base64 kernels can be built from, runs 8
+// independent dependency chains per lane (a = op(a, b, c), b and c loop
+// invariant), 8 waves per SIMD on every CU, and reports wave64 lane-ops/s.
+// The survey's roofline denominator (256 CU x 4 SIMD x 32 lanes x 2.4 GHz)
+// is printed beside it as clock_peak_ops.
 //   build: hipcc -O3 --offload-arch=gfx950 tools/valu_peak.hip -o tools/valu_peak
 //   run:   tools/valu_peak  -> one JSON line
 #include <hip/hip_runtime.h>
 #include <cstdio>
-#include <cstdlib>
 
-#define CHAINS 8
-constexpr int kIters = 4096;
+constexpr int kIters = 2048;
+constexpr int kChains = 8;
+constexpr int kUnroll = 8;
 
-template <int OP>
+#define DEFOP(NAME, ASM)                                                           \
+    struct NAME {                                                                  \
+        static constexpr const char* name = #NAME;                                 \
+        static __device__ __forceinline__ void f(uint32_t& a, uint32_t b, uint32_t c) { \
+            asm volatile(ASM : "+v"(a) : "v"(b), "v"(c));                          \
+        }                                                                          \
+    };
+
+DEFOP(add3, "v_add3_u32 %0, %0, %1, %2")
+DEFOP(alignbit, "v_alignbit_b32 %0, %0, %1, 7")
+DEFOP(alignbit_rot, "v_alignbit_b32 %0, %0, %0, 7")
+DEFOP(bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96")
+DEFOP(add, "v_add_u32_e32 %0, %0, %1")
+DEFOP(xor2, "v_xor_b32_e32 %0, %0, %1")
+DEFOP(lshr, "v_lshrrev_b32_e32 %0, 7, %0")
+DEFOP(lshl_or, "v_lshl_or_b32 %0, %0, 7, %1")
+DEFOP(lshl_add, "v_lshl_add_u32 %0, %0, 3, %1")
+DEFOP(xad, "v_xad_u32 %0, %0, %1, %2")
+DEFOP(perm, "v_perm_b32 %0, %0, %1, %2")
+DEFOP(alignbyte, "v_alignbyte_b32 %0, %0, %1, 1")
+DEFOP(bfi, "v_bfi_b32 %0, %0, %1, %2")
+DEFOP(or3, "v_or3_b32 %0, %0, %1, %2")
+DEFOP(and_or, "v_and_or_b32 %0, %0, %1, %2")
+DEFOP(pk_add_u16, "v_pk_add_u16 %0, %0, %1")
+DEFOP(bfe, "v_bfe_u32 %0, %0, 6, 6")
+DEFOP(mad_u24, "v_mad_u32_u24 %0, %0, %1, %2")
+
+template <class OP>
 __global__ __launch_bounds__(256) void chains(uint32_t* out, uint32_t seed) {
-    uint32_t v[CHAINS];
+    uint32_t v[kChains];
 #pragma unroll
-    for (int c = 0; c < CHAINS; ++c) v[c] = seed * (threadIdx.x + 1) + c * 0x9e3779b9u + blockIdx.x;
+    for (int c = 0; c < kChains; ++c) v[c] = seed * (threadIdx.x + 1) + c * 0x9e3779b9u + blockIdx.x;
+    const uint32_t b = seed ^ threadIdx.x, cc = seed + 0x01020304u;
     for (int i = 0; i < kIters; ++i) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < kUnroll; ++u) {
 #pragma unroll
-            for (int c = 0; c < CHAINS; ++c) {
-                if (OP == 0) v[c] = v[c] + v[(c + 1) % CHAINS] + 0x1234567u;  // folds to v_add3
-                if (OP == 1) v[c] = __builtin_amdgcn_alignbit(v[c], v[(c + 1) % CHAINS], 7 + u);
-                if (OP == 2) v[c] = __builtin_amdgcn_bitop3_b32(v[c], v[(c + 1) % CHAINS], v[(c + 3) % CHAINS], 0x96);
-                if (OP == 3) v[c] = v[c] + v[(c + 5) % CHAINS];
-            }
+            for (int c = 0; c < kChains; ++c) OP::f(v[c], b, cc);
         }
     }
     uint32_t r = 0;
 #pragma unroll
-    for (int c = 0; c < CHAINS; ++c) r ^= v[c];
+    for (int c = 0; c < kChains; ++c) r ^= v[c];
     out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
-template <int OP>
-double run(uint32_t* d, int blocks) {
+template <class OP>
+void run(uint32_t* d, int blocks, bool comma) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
@@ -50,21 +73,39 @@ double run(uint32_t* d, int blocks) {
     (void)hipEventSynchronize(b);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, a, b);
-    const double ops = 1.0 * reps * blocks * 256.0 * kIters * 8 * CHAINS;
-    return ops / (ms * 1e-3);
+    const double ops = 1.0 * reps * blocks * 256.0 * kIters * kUnroll * kChains;
+    std::printf("%s\"%s\": %.4g", comma ? ", " : "", OP::name, ops / (ms * 1e-3));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
 }
 
 int main() {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, 0) != hipSuccess) return 1;
-    const int blocks = p.multiProcessorCount * 8;  // 8 waves/SIMD
+    const int blocks = p.multiProcessorCount * 8;  // 8 waves per SIMD
     uint32_t* d;
-    (void)hipMalloc(&d, sizeof(uint32_t) * blocks * 256);
-    const double add3 = run<0>(d, blocks), align = run<1>(d, blocks), bop = run<2>(d, blocks), add = run<3>(d, blocks);
-    std::printf("{\"cus\": %d, \"clock_mhz\": %d, \"add3_ops\": %.4g, \"alignbit_ops\": %.4g, \"bitop3_ops\": %.4g, "
-                "\"add_ops\": %.4g, \"clock_peak_ops\": %.4g}\n",
-                p.multiProcessorCount, p.clockRate / 1000, add3, align, bop, add,
-                p.multiProcessorCount * 4.0 * 32.0 * p.clockRate * 1e3);
+    if (hipMalloc(&d, sizeof(uint32_t) * blocks * 256) != hipSuccess) return 1;
+    std::printf("{\"cus\": %d, \"clock_mhz\": %d, \"clock_peak_ops\": %.4g, \"ops\": {", p.multiProcessorCount,
+                p.clockRate / 1000, p.multiProcessorCount * 4.0 * 32.0 * p.clockRate * 1e3);
+    run<add3>(d, blocks, false);
+    run<alignbit>(d, blocks, true);
+    run<alignbit_rot>(d, blocks, true);
+    run<bitop3>(d, blocks, true);
+    run<add>(d, blocks, true);
+    run<xor2>(d, blocks, true);
+    run<lshr>(d, blocks, true);
+    run<lshl_or>(d, blocks, true);
+    run<lshl_add>(d, blocks, true);
+    run<xad>(d, blocks, true);
+    run<perm>(d, blocks, true);
+    run<alignbyte>(d, blocks, true);
+    run<bfi>(d, blocks, true);
+    run<or3>(d, blocks, true);
+    run<and_or>(d, blocks, true);
+    run<pk_add_u16>(d, blocks, true);
+    run<bfe>(d, blocks, true);
+    run<mad_u24>(d, blocks, true);
+    std::printf("}}\n");
     (void)hipFree(d);
     return 0;
 }
