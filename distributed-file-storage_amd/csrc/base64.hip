@@ -289,10 +289,10 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
 }  // namespace
 
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, char* out,
-                             hipStream_t s) {
+                             uint32_t wgs_per_cu, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(b64_encode_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, base, jobs, njobs,
-                       ntiles, out);
+    hipLaunchKernelGGL(b64_encode_kernel, dim3(stream_grid(ntiles, wgs_per_cu)), dim3(kStreamBlock), 0, s, base, jobs,
+                       njobs, ntiles, out);
     return hipGetLastError();
 }
 

@@ -82,7 +82,10 @@ __device__ __forceinline__ void load_block(const uint32_t* __restrict__ p, uint3
         const uint4 v = q[i];
         r[4 * i + 0] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
     }
-    x = sh ? p[16] : 0u;
+    // Always 5 loads, no branch (a conditional load makes hipcc's counted
+    // s_waitcnt wait for the fresh prefetch).  For sh == 0 the look-ahead
+    // word is not needed and p[16] may lie past the message: re-read p[15].
+    x = p[sh ? 16 : 15];
 }
 
 // In place: r[j] <- big-endian word at byte offset sh of {r[j], r[j+1]}.
@@ -90,6 +93,69 @@ __device__ __forceinline__ void to_be(uint32_t (&r)[16], uint32_t x, uint32_t se
 #pragma unroll
     for (int j = 0; j < 15; ++j) r[j] = __builtin_amdgcn_perm(r[j + 1], r[j], sel);
     r[15] = __builtin_amdgcn_perm(x, r[15], sel);
+}
+
+// Per-lane message geometry.
+struct Msg {
+    const uint32_t* p;  // dword-aligned pointer at or below the first byte
+    uint64_t len;
+    uint32_t sh, sel, nfull, ntb, out;
+};
+
+__device__ __forceinline__ Msg msg_setup(const uint8_t* __restrict__ base, const ShaDesc& d) {
+    Msg m;
+    m.sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(base + d.off)) & 3u;
+    m.p = reinterpret_cast<const uint32_t*>(base + d.off - m.sh);
+    m.sel = (m.sh + 3u) | ((m.sh + 2u) << 8) | ((m.sh + 1u) << 16) | (m.sh << 24);
+    m.len = d.len;
+    m.nfull = static_cast<uint32_t>(d.len >> 6);
+    m.ntb = (static_cast<uint32_t>(d.len) & 63u) < 56u ? 1u : 2u;
+    m.out = d.out;
+    return m;
+}
+
+// Tail block tb (0 or 1) of a message: the last len mod 64 bytes, the 0x80
+// pad byte, zeros and (in the final block) the 64-bit big-endian bit length
+// (FIPS 180-4 §5.1.1).  Loads are guarded: a dword is read only if it holds
+// at least one message byte.
+__device__ __forceinline__ void tail_block(const Msg& m, uint32_t tb, uint32_t (&W)[16]) {
+    const uint32_t r = static_cast<uint32_t>(m.len) & 63u;
+    const uint32_t lim = m.len ? m.sh + r : 0u;  // tail word i holds message bytes iff 4i < lim
+    const uint32_t* __restrict__ q = m.p + 16u * m.nfull;
+    uint32_t T[17];
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+        const uint32_t wi = 16u * tb + static_cast<uint32_t>(i);
+        T[i] = (4u * wi < lim) ? q[wi] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int rem = static_cast<int>(r) - 64 * static_cast<int>(tb) - 4 * j;  // message bytes in word j
+        const uint32_t w = __builtin_amdgcn_perm(T[j + 1], T[j], m.sel);
+        const uint32_t mask = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
+        const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
+        W[j] = (w & mask) | pad;
+    }
+    if (tb + 1u == m.ntb) {
+        const uint64_t bits = m.len << 3;
+        W[14] = static_cast<uint32_t>(bits >> 32);
+        W[15] = static_cast<uint32_t>(bits);
+    }
+}
+
+__device__ __forceinline__ void store_digest(const uint32_t (&st)[8], uint32_t out, uint32_t split,
+                                             uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
+    uint8_t* dst = out < split ? out0 + 32ull * out : out1 + 32ull * (out - split);
+    uint4* o = reinterpret_cast<uint4*>(dst);
+    o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                      __builtin_bswap32(st[3]));
+    o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                      __builtin_bswap32(st[7]));
+}
+
+__device__ __forceinline__ void init_state(uint32_t (&st)[8]) {
+    st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
+    st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
 }
 
 __device__ __forceinline__ uint32_t hw_id() {
@@ -157,62 +223,31 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
         if (census) t_start = __builtin_amdgcn_s_memrealtime();
         const uint32_t gid = item * 64u + lane;
         if (gid < n) {
-            const ShaDesc d = descs[gid];
-            const uint32_t sh = static_cast<uint32_t>(d.off) & 3u;
-            const uint32_t* __restrict__ p = reinterpret_cast<const uint32_t*>(base + (d.off - sh));
-            const uint32_t sel = (sh + 3u) | ((sh + 2u) << 8) | ((sh + 1u) << 16) | (sh << 24);
-            const uint32_t nfull = static_cast<uint32_t>(d.len >> 6);
-            uint32_t st[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
-                              0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
-            if (nfull) {
+            const Msg m = msg_setup(base, descs[gid]);
+            uint32_t st[8];
+            init_state(st);
+            if (m.nfull) {
                 uint32_t A[16], B[16], xa, xb;
-                load_block(p, sh, A, xa);
+                load_block(m.p, m.sh, A, xa);
                 uint32_t k = 0;
                 for (;;) {
                     // A holds block k; prefetch block k+1 (clamped) into B.
-                    load_block(p + 16u * min(k + 1u, nfull - 1u), sh, B, xb);
-                    to_be(A, xa, sel);
+                    load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, B, xb);
+                    to_be(A, xa, m.sel);
                     compress(st, A);
-                    if (++k >= nfull) break;
-                    load_block(p + 16u * min(k + 1u, nfull - 1u), sh, A, xa);
-                    to_be(B, xb, sel);
+                    if (++k >= m.nfull) break;
+                    load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, A, xa);
+                    to_be(B, xb, m.sel);
                     compress(st, B);
-                    if (++k >= nfull) break;
+                    if (++k >= m.nfull) break;
                 }
             }
-            // Tail: r = len mod 64 bytes + FIPS 180-4 §5.1.1 padding, 1 or 2 blocks.
-            const uint32_t r = static_cast<uint32_t>(d.len) & 63u;
-            const uint64_t bits = d.len << 3;
-            const uint32_t ntb = r < 56u ? 1u : 2u;
-            const uint32_t lim = d.len ? sh + r : 0u;  // word i of the tail holds message bytes iff 4i < lim
-            const uint32_t* __restrict__ q = p + 16u * nfull;
-            for (uint32_t tb = 0; tb < ntb; ++tb) {
-                uint32_t T[17], W[16];
-#pragma unroll
-                for (int i = 0; i < 17; ++i) {
-                    const uint32_t wi = 16u * tb + static_cast<uint32_t>(i);
-                    T[i] = (4u * wi < lim) ? q[wi] : 0u;
-                }
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int rem = static_cast<int>(r) - 64 * static_cast<int>(tb) - 4 * j;  // message bytes in word j
-                    const uint32_t w = __builtin_amdgcn_perm(T[j + 1], T[j], sel);
-                    const uint32_t mask = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
-                    const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80000000u >> (8 * rem)) : 0u;
-                    W[j] = (w & mask) | pad;
-                }
-                if (tb + 1u == ntb) {
-                    W[14] = static_cast<uint32_t>(bits >> 32);
-                    W[15] = static_cast<uint32_t>(bits);
-                }
+            for (uint32_t tb = 0; tb < m.ntb; ++tb) {
+                uint32_t W[16];
+                tail_block(m, tb, W);
                 compress(st, W);
             }
-            uint8_t* dst = d.out < split ? out0 + 32ull * d.out : out1 + 32ull * (d.out - split);
-            uint4* o = reinterpret_cast<uint4*>(dst);
-            o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
-                              __builtin_bswap32(st[3]));
-            o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
-                              __builtin_bswap32(st[7]));
+            store_digest(st, m.out, split, out0, out1);
         }
         if (census && lane == 0u) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
@@ -225,7 +260,89 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
     }
 }
 
+// Lane sequences: lane l hashes messages seq[l] .. seq[l+1]-1 one after the
+// other, one 64-byte block per loop iteration, with a single compress body.
+// The upload plan pairs, in one wave, the fileId lane of file f (lanes
+// 0..31) with a lane that hashes f's N fragments in order (lanes 32..63):
+// at every iteration both lanes read within 64 bytes of each other in the
+// file, so the second read hits the line the first one brought in (the file
+// crosses HBM once for both chains), and every wave runs the same
+// ceil((S+9)/64)-ish iterations.  Messages switch at per-lane tail blocks
+// (rare, exec-masked branches).
+__device__ __forceinline__ void sha256_seq_lane(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
+                                                const uint32_t* __restrict__ seq, uint32_t l, uint32_t split,
+                                                uint8_t* __restrict__ out0, uint8_t* __restrict__ out1);
+
+__global__ __launch_bounds__(kShaBlock) void sha256_seq(const uint8_t* __restrict__ base,
+                                                        const ShaDesc* __restrict__ descs,
+                                                        const uint32_t* __restrict__ seq, uint32_t nlanes,
+                                                        uint32_t split, uint8_t* __restrict__ out0,
+                                                        uint8_t* __restrict__ out1, uint32_t* __restrict__ census) {
+    const uint32_t l = blockIdx.x * kShaBlock + threadIdx.x;
+    const uint64_t t_start = census ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (l < nlanes) sha256_seq_lane(base, descs, seq, l, split, out0, out1);
+    if (census && (threadIdx.x & 63u) == 0u) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t* c = census + 4ull * (l >> 6);
+        c[0] = hw_id();
+        c[1] = xcc_id();
+        c[2] = static_cast<uint32_t>(t_start);
+        c[3] = static_cast<uint32_t>(t_end);
+    }
+}
+
+__device__ __forceinline__ void sha256_seq_lane(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
+                                                const uint32_t* __restrict__ seq, uint32_t l, uint32_t split,
+                                                uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
+    uint32_t mi = seq[l];
+    const uint32_t mend = seq[l + 1];
+    if (mi >= mend) return;
+    Msg m = msg_setup(base, descs[mi]);
+    uint32_t st[8];
+    init_state(st);
+    uint32_t A[16], B[16], xa = 0, xb = 0;
+    if (m.nfull) load_block(m.p, m.sh, A, xa);
+    uint32_t k = 0;
+    // Two register buffers in ping-pong (the loop body is written twice so no
+    // register copy ever waits on the prefetch): CUR holds block k, NXT
+    // receives block k+1 (or block 0 of the lane's next message).
+#define DFS_SHA_SEQ_STEP(CUR, XC, NXT, XN)                                              \
+    {                                                                                   \
+        uint32_t W[16];                                                                 \
+        if (k < m.nfull) {                                                              \
+            load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, NXT, XN);           \
+            _Pragma("unroll") for (int i = 0; i < 16; ++i) W[i] = CUR[i];               \
+            to_be(W, XC, m.sel);                                                        \
+        } else {                                                                        \
+            tail_block(m, k - m.nfull, W);                                              \
+        }                                                                               \
+        compress(st, W);                                                                \
+        if (++k == m.nfull + m.ntb) { /* message done: publish, start the next one */  \
+            store_digest(st, m.out, split, out0, out1);                                 \
+            if (++mi >= mend) break;                                                    \
+            m = msg_setup(base, descs[mi]);                                             \
+            init_state(st);                                                             \
+            k = 0;                                                                      \
+            if (m.nfull) load_block(m.p, m.sh, NXT, XN);                                \
+        }                                                                               \
+    }
+    for (;;) {
+        DFS_SHA_SEQ_STEP(A, xa, B, xb)
+        DFS_SHA_SEQ_STEP(B, xb, A, xa)
+    }
+#undef DFS_SHA_SEQ_STEP
+}
+
 }  // namespace
+
+hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const uint32_t* seq, uint32_t nlanes,
+                             uint32_t split, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s) {
+    if (nlanes == 0) return hipSuccess;
+    const uint32_t grid = (nlanes + kShaBlock - 1) / kShaBlock;
+    hipLaunchKernelGGL(sha256_seq, dim3(grid), dim3(kShaBlock), 0, s, base, descs, seq, nlanes, split, out0, out1,
+                       census);
+    return hipGetLastError();
+}
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,

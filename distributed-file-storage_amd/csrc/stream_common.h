@@ -29,10 +29,11 @@ __device__ __forceinline__ void tile_range(uint64_t ntiles, uint64_t& t0, uint64
     t1 = ntiles * (b + 1) / g;
 }
 
-// Grid size for a tile count: enough workgroups to fill 256 CUs several
-// times over, never more than the tiles.
-inline uint32_t stream_grid(uint64_t ntiles) {
-    const uint64_t cap = 256ull * 8;
+// Grid size for a tile count: wgs_per_cu workgroups (4 waves each) on each of
+// the 256 CUs, never more than the tiles.  The encode kernel that runs beside
+// the SHA kernel leaves 2 waves/SIMD free for it (wgs_per_cu = 6).
+inline uint32_t stream_grid(uint64_t ntiles, uint32_t wgs_per_cu = 8) {
+    const uint64_t cap = 256ull * wgs_per_cu;
     return static_cast<uint32_t>(ntiles < cap ? (ntiles ? ntiles : 1) : cap);
 }
 
