@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     ap.add_argument("--verify", type=int, default=8, help="files spot-checked against the oracle (rank 0)")
+    ap.add_argument("--no-replicate", action="store_true", help="N>1: skip the placement / degraded-read leg")
+    ap.add_argument("--rep-files", type=int, default=8192, help="files per GPU in the placement leg")
+    ap.add_argument("--rep-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -95,6 +98,85 @@ def cpu_baseline(args, log):
                       f" + scalar Base64, one file per thread (thread-per-connection, SN:30); "
                       f"CPU proxy, not Java (no JDK on the box)",
             "seconds": round(secs, 3)}
+
+
+def replication_leg(args, eng, files, S, N, dev, log):
+    """N>1 only: place a bounded sample of this rank's fragments on the GPUs
+    hosting their nodes (primary scatter + replica step over RCCL/xGMI,
+    dfs_amd.placement), then run config 5's degraded download with the last
+    rank offline: fetch from the surviving holders, Base64-decode into place,
+    per-fragment and fileId SHA-256 verify (dfs_download_batch).  Timed
+    separately from the compute steps; returns a dict for the JSON line."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import dfs_amd
+    from dfs_amd import placement as P
+    from dfs_amd.engine import download_device
+    world, me = dist.get_world_size(), dist.get_rank()
+    R = min(args.files, args.rep_files)
+    spans = np.stack([np.arange(R, dtype=np.uint64) * np.uint64(S), np.full(R, S, dtype=np.uint64)], axis=1)
+    plan = dfs_amd.UploadPlan(eng, spans, N, frag_major=True)
+    fd = torch.empty(R * 32, dtype=torch.uint8, device=dev)
+    frd = torch.empty(R * N * 32, dtype=torch.uint8, device=dev)
+    b64 = torch.empty(plan.b64_total, dtype=torch.uint8, device=dev)
+    plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), dfs_amd.DFS_SERIAL)
+    torch.cuda.synchronize(dev)
+    offs = plan.b64_offsets()
+    group_off = [int(offs[i]) for i in range(N)] + [int(offs[-1])]
+
+    def timed(fn, reps):
+        fn()  # warm-up
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return r, float(tt.item()) / reps
+
+    (held, table), t_up = timed(lambda: P.exchange_upload(b64, group_off, N), args.rep_steps)
+    sent = sum(table[me][f] for f in range(N) if P.node_gpu(f, world) != me)
+    sent += sum(sum(table[r][f] for r in range(world)) for f in range(N)
+                if P.node_gpu(f, world) == me and P.node_gpu(P.fragment_holders(f, N)[1], world) != me)
+    sent_t = torch.tensor([sent], dtype=torch.float64, device=dev)
+    dist.all_reduce(sent_t)
+    ok_ex = all(len(held[f][0]) == sum(table[r][f] for r in range(world)) for f in P.gpu_fragments(me, N, world))
+
+    offline = {world - 1}
+    fetched, t_fetch = timed(lambda: P.exchange_download(held, table, N, offline=offline, device=dev), args.rep_steps)
+    result = {"files_per_gpu": R, "nodes": N, "node_to_gpu": "node k on GPU k mod W",
+              "upload_exchange_ms": round(t_up * 1e3, 3),
+              "upload_exchange_gbps_per_gpu": round(sent_t.item() / world / t_up / 1e9, 2),
+              "exchange_sizes_ok": bool(ok_ex), "offline_gpu": world - 1,
+              "degraded_fetch_ms": round(t_fetch * 1e3, 3)}
+    status_ok = True
+    if me not in offline:
+        # one contiguous Base64 buffer, spans per (file, fragment)
+        groups = [fetched[f] for f in range(N)]
+        status_ok = all(g is not None for g in groups)
+        if status_ok:
+            blob = torch.cat(groups)
+            msp = P.frag_major_spans([S] * R, N)
+            out = torch.empty(R * S, dtype=torch.uint8, device=dev)
+            file_len = np.full(R, S, dtype=np.uint64)
+            file_off = np.arange(R, dtype=np.uint64) * np.uint64(S)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            status = download_device(eng, blob.data_ptr(), msp, R, N, file_len, frd.data_ptr(), fd.data_ptr(),
+                                     out.data_ptr(), file_off)
+            t_dl = time.perf_counter() - t0
+            status_ok = bool((status == 0).all()) and bool(torch.equal(out, files[:R * S]))
+            result["degraded_download_ms"] = round(t_dl * 1e3, 3)
+            result["degraded_download_gbps"] = round(R * S / t_dl / 1e9, 2)
+    flag = torch.tensor([1 if status_ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    result["degraded_download_ok"] = bool(flag.item())
+    plan.close()
+    return result
 
 
 def main():
@@ -223,6 +305,11 @@ def main():
                          "ms": round(b64_avg * 1e3, 3), "bytes_per_launch": b64_bytes},
         "verified": ok,
     }
+    if world > 1 and not args.no_replicate:
+        try:
+            result["replication"] = replication_leg(args, eng, files, S, N, dev, log)
+        except Exception as e:  # never lose the main line to the side measurement
+            result["replication"] = {"error": repr(e)[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, log)
     if rank == 0:

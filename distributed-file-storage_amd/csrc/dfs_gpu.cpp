@@ -117,6 +117,9 @@ void split(uint64_t S, uint32_t N, uint64_t* off, uint64_t* len) {
 
 uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
 
+// A whole message (not resumed): len bytes at off, digest slot out.
+ShaDesc msg(uint64_t off, uint64_t len, uint64_t out) { return ShaDesc{off, len, len, static_cast<uint32_t>(out), 0}; }
+
 // Sort SHA lanes longest-first (uniform waves) and count the lanes that
 // carry the long chains: those waves get issue priority in the kernel.
 uint32_t sort_lanes(std::vector<ShaDesc>& d) {
@@ -347,7 +350,7 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
     uint64_t end = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (msgs[i].len >= kMaxMsg) return DFS_E_ARG;
-        d[i] = ShaDesc{msgs[i].off, msgs[i].len, i, 0};
+        d[i] = msg(msgs[i].off, msgs[i].len, i);
         end = std::max(end, msgs[i].off + msgs[i].len);
     }
     if (end && !base) return DFS_E_ARG;
@@ -373,6 +376,98 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
         HIPC(hipStreamSynchronize(s));
     }
     return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_sha256_update_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* parts, uint32_t n, uint32_t* state,
+                            const uint64_t* total_len, uint8_t* digests, uint32_t flags) {
+    const bool begin = flags & DFS_SHA_BEGIN, fin = flags & DFS_SHA_FINAL;
+    if (!c || (n && (!parts || !state || (fin && (!total_len || !digests))))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!n) return DFS_OK;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    hipStream_t s = c->stream();
+    std::vector<ShaDesc> d(n);
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (parts[i].len >= kMaxMsg || (!fin && (parts[i].len & 63u))) return DFS_E_ARG;
+        if (fin && total_len[i] < parts[i].len) return DFS_E_ARG;
+        d[i] = ShaDesc{parts[i].off, parts[i].len, fin ? total_len[i] : parts[i].len, i,
+                       (begin ? 0u : dfs::kShaResume) | (fin ? 0u : dfs::kShaPartial)};
+        end = std::max(end, parts[i].off + parts[i].len);
+    }
+    if (end && !base) return DFS_E_ARG;
+    const uint32_t prio = sort_lanes(d);
+    const uint8_t* d_base = base;
+    uint32_t* d_state = state;
+    uint8_t* d_dig = digests;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, base, end, s)) return rc;
+        d_base = c->buf[B_DATA_IN].as<uint8_t>();
+        if (int rc = put(c, B_STATUS, state, begin ? 0 : 32ull * n, s)) return rc;
+        HIPC(c->buf[B_STATUS].ensure(32ull * n));
+        d_state = c->buf[B_STATUS].as<uint32_t>();
+        HIPC(c->buf[B_DIG0].ensure(32ull * n));
+        d_dig = c->buf[B_DIG0].as<uint8_t>();
+    }
+    if (int rc = put(c, B_DESC, d.data(), d.size() * sizeof(ShaDesc), s)) return rc;
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_SHA, s);
+    HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, d_state));
+    tm.end(DFS_T_SHA, s);
+    tm.end(DFS_T_TOTAL, s);
+    if (!dev) {
+        if (fin) HIPC(hipMemcpyAsync(digests, d_dig, 32ull * n, hipMemcpyDeviceToHost, s));
+        else HIPC(hipMemcpyAsync(state, d_state, 32ull * n, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
+int dfs_receive_fragments_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint32_t n, uint8_t* out,
+                                const uint64_t* out_off, uint64_t* out_len, uint8_t* digests, int32_t* status,
+                                uint32_t flags) {
+    if (!c || (n && (!digests || !out_len || !status))) return DFS_E_ARG;
+    // Decode (SN:281); the decode call synchronises and fills out_len / status.
+    int rc = dfs_b64_decode_batch(c, in, msgs, n, out, out_off, out_len, status, flags);
+    if (rc != DFS_OK && rc != DFS_E_DECODE) return rc;
+    std::vector<dfs_span> ok;
+    std::vector<uint32_t> idx;
+    for (uint32_t i = 0; i < n; ++i)
+        if (status[i] == DFS_OK) {
+            ok.push_back(dfs_span{out_off[i], out_len[i]});
+            idx.push_back(i);
+        }
+    if (ok.empty()) return rc;
+    // Hash the decoded bytes where they landed (SN:282).
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    std::vector<uint8_t> dig(32ull * ok.size());
+    if (dev) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (int e = enter(c)) return e;
+        hipStream_t s = c->stream();
+        std::vector<ShaDesc> d(ok.size());
+        for (size_t k = 0; k < ok.size(); ++k) d[k] = msg(ok[k].off, ok[k].len, k);
+        const uint32_t prio = sort_lanes(d);
+        HIPC(c->buf[B_DIG1].ensure(dig.size()));
+        if (int e = put(c, B_DESC, d.data(), d.size() * sizeof(ShaDesc), s)) return e;
+        HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+        HIPC(dfs::launch_sha256(out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(d.size()),
+                                static_cast<uint32_t>(d.size()), prio, c->buf[B_DIG1].as<uint8_t>(),
+                                c->buf[B_DIG1].as<uint8_t>(), c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr,
+                                s));
+        HIPC(hipMemcpyAsync(dig.data(), c->buf[B_DIG1].p, dig.size(), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    } else {
+        if (int e = dfs_sha256_batch(c, out, ok.data(), static_cast<uint32_t>(ok.size()), dig.data(), 0)) return e;
+    }
+    for (size_t k = 0; k < idx.size(); ++k) std::memcpy(digests + 32ull * idx[k], dig.data() + 32 * k, 32);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -492,9 +587,11 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
 
 // ---------------------------------------------------------------------------
 // Upload plan: descriptors built once on the host, uploaded once.
-int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, uint32_t nfrag,
+int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint32_t flags,
                            dfs_upload_plan** out, uint64_t* b64_total) {
     if (!c || !out || !nfrag || (nfiles && !files)) return DFS_E_ARG;
+    if (flags & ~DFS_LAYOUT_FRAG_MAJOR) return DFS_E_ARG;
+    const bool frag_major = flags & DFS_LAYOUT_FRAG_MAJOR;
     *out = nullptr;
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = enter(c)) return rc;
@@ -517,31 +614,43 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     items.reserve(nf);
     p->b64_off.resize(nf + 1);
     std::vector<uint64_t> off(nfrag), len(nfrag);
-    uint64_t total = 0;
     for (uint32_t f = 0; f < nfiles; ++f) {
         if (files[f].len >= kMaxMsg) {
             delete p;
             return DFS_E_ARG;
         }
-        all.push_back(ShaDesc{files[f].off, files[f].len, f, 0});  // fileId, SN:127
+        all.push_back(msg(files[f].off, files[f].len, f));  // fileId, SN:127
         split(files[f].len, nfrag, off.data(), len.data());          // SN:138-157
         for (uint32_t i = 0; i < nfrag; ++i) {
             const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
-            const ShaDesc d{files[f].off + off[i], len[i], static_cast<uint32_t>(nfiles + k), 0};  // SN:159
+            const ShaDesc d = msg(files[f].off + off[i], len[i], nfiles + k);  // SN:159
             all.push_back(d);
             frag.push_back(d);
-            p->b64_off[k] = total;
-            if (len[i]) {
-                StreamJob j{};
-                j.src_off = files[f].off + off[i];
-                j.len = len[i];
-                j.dst_off = total;
-                j.id = static_cast<uint32_t>(k);
-                enc.push_back(j);
-                items.push_back((len[i] + 11) / 12);
-            }
-            total += enc_len(len[i]);  // SN:636
         }
+    }
+    // Base64 layout: [file][fragment] (default) or [fragment][file].
+    uint64_t total = 0;
+    auto place = [&](uint32_t f, uint32_t i) {
+        const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+        const ShaDesc& d = frag[k];
+        p->b64_off[k] = total;
+        if (d.len) {
+            StreamJob j{};
+            j.src_off = d.off;
+            j.len = d.len;
+            j.dst_off = total;
+            j.id = static_cast<uint32_t>(k);
+            enc.push_back(j);
+            items.push_back((d.len + 11) / 12);
+        }
+        total += enc_len(d.len);  // SN:636
+    };
+    if (frag_major) {
+        for (uint32_t i = 0; i < nfrag; ++i)
+            for (uint32_t f = 0; f < nfiles; ++f) place(f, i);
+    } else {
+        for (uint32_t f = 0; f < nfiles; ++f)
+            for (uint32_t i = 0; i < nfrag; ++i) place(f, i);
     }
     p->b64_off[nf] = total;
     p->b64_total = total;
@@ -554,12 +663,11 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     std::vector<ShaDesc> pair;
     std::vector<uint32_t> seq;
     build_pairs(
-        nfiles, nfrag, [&](uint32_t f) { return ShaDesc{files[f].off, files[f].len, f, 0}; },
+        nfiles, nfrag, [&](uint32_t f) { return msg(files[f].off, files[f].len, f); },
         [&](uint32_t f, uint32_t i) {
             const uint64_t base = files[f].len / nfrag, rem = files[f].len % nfrag;
             const uint64_t o = i * base + (i < rem ? i : rem);
-            return ShaDesc{files[f].off + o, base + (i < rem ? 1 : 0),
-                           static_cast<uint32_t>(nfiles + static_cast<uint64_t>(f) * nfrag + i), 0};
+            return msg(files[f].off + o, base + (i < rem ? 1 : 0), nfiles + static_cast<uint64_t>(f) * nfrag + i);
         },
         pair, seq);
     p->n_seq_lanes = static_cast<uint32_t>(seq.size() - 1);
@@ -684,7 +792,7 @@ int dfs_upload_batch(dfs_ctx* c, const uint8_t* files, const dfs_span* spans, ui
     if (!(flags & DFS_NO_FILEID) && nfiles && !fd) return DFS_E_ARG;
     dfs_upload_plan* p = nullptr;
     uint64_t total = 0;
-    if (int rc = dfs_upload_plan_create(c, spans, nfiles, nfrag, &p, &total)) return rc;
+    if (int rc = dfs_upload_plan_create(c, spans, nfiles, nfrag, flags & DFS_LAYOUT_FRAG_MAJOR, &p, &total)) return rc;
     struct Guard {
         dfs_upload_plan* p;
         ~Guard() { dfs_upload_plan_destroy(p); }
@@ -787,7 +895,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
             }
             o += frag_len[k];
         }
-        sha.push_back(ShaDesc{file_off[f], flen[f], f, 0});  // SN:454
+        sha.push_back(msg(file_off[f], flen[f], f));  // SN:454
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
     const uint64_t ntiles = finish_jobs(jobs, items, dfs::kCopyChunksPerTile);
@@ -870,9 +978,9 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
             j.id = static_cast<uint32_t>(k);
             jobs.push_back(j);
             items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
-            sha.push_back(ShaDesc{file_off[f] + off[i], len[i], static_cast<uint32_t>(k), 0});
+            sha.push_back(msg(file_off[f] + off[i], len[i], k));
         }
-        sha.push_back(ShaDesc{file_off[f], file_len[f], static_cast<uint32_t>(nf + f), 0});
+        sha.push_back(msg(file_off[f], file_len[f], nf + f));
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
     const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecChunksPerTile);
@@ -889,14 +997,13 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
             static_cast<uint32_t>(valid.size()), nfrag,
             [&](uint32_t v) {
                 const uint32_t f = valid[v];
-                return ShaDesc{file_off[f], file_len[f], static_cast<uint32_t>(nf + f), 0};
+                return msg(file_off[f], file_len[f], nf + f);
             },
             [&](uint32_t v, uint32_t i) {
                 const uint32_t f = valid[v];
                 const uint64_t b = file_len[f] / nfrag, rem = file_len[f] % nfrag;
                 const uint64_t o = i * b + (i < rem ? i : rem);
-                return ShaDesc{file_off[f] + o, b + (i < rem ? 1 : 0),
-                               static_cast<uint32_t>(static_cast<uint64_t>(f) * nfrag + i), 0};
+                return msg(file_off[f] + o, b + (i < rem ? 1 : 0), static_cast<uint64_t>(f) * nfrag + i);
             },
             sha, seq);
     } else {

@@ -11,10 +11,17 @@ namespace dfs {
 // digest goes to out0 + 32*out (out < split) or out1 + 32*(out - split).
 struct ShaDesc {
     uint64_t off;
-    uint64_t len;
+    uint64_t len;    // bytes hashed by this lane in this launch
+    uint64_t total;  // whole-message length (the padding's bit count); = len unless resumed
     uint32_t out;
-    uint32_t pad;
+    uint32_t flags;  // kShaResume / kShaPartial
 };
+// Streaming (SHA-256 update across launches, e.g. the 256 MiB skew config):
+// kShaResume: start from the 8-word state in state[8*out] instead of H0;
+// kShaPartial: len is a multiple of 64 and the message continues: store the
+// running state to state[8*out] instead of padding and emitting a digest.
+constexpr uint32_t kShaResume = 1u;
+constexpr uint32_t kShaPartial = 2u;
 
 // One byte-stream job for the tiled HBM-bound kernels (Base64 encode/decode,
 // gather, synth).  Jobs are sorted by tile_start; a sentinel job with
@@ -48,7 +55,7 @@ inline uint64_t enc_tiles(uint64_t len) {
 // on each of the 1024 SIMDs (fewer for small batches).
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
-                         int waves_per_simd, uint32_t* census, hipStream_t s);
+                         int waves_per_simd, uint32_t* census, hipStream_t s, uint32_t* state = nullptr);
 // Lane-sequence SHA-256: lane l hashes descs[seq[l] .. seq[l+1]) in order.
 hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const uint32_t* seq, uint32_t nlanes,
                              uint32_t split, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s);

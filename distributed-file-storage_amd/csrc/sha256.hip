@@ -98,8 +98,9 @@ __device__ __forceinline__ void to_be(uint32_t (&r)[16], uint32_t x, uint32_t se
 // Per-lane message geometry.
 struct Msg {
     const uint32_t* p;  // dword-aligned pointer at or below the first byte
-    uint64_t len;
-    uint32_t sh, sel, nfull, ntb, out;
+    uint64_t len;       // bytes of this part
+    uint64_t total;     // whole-message length (padding bit count)
+    uint32_t sh, sel, nfull, ntb, out, flags;
 };
 
 __device__ __forceinline__ Msg msg_setup(const uint8_t* __restrict__ base, const ShaDesc& d) {
@@ -108,9 +109,11 @@ __device__ __forceinline__ Msg msg_setup(const uint8_t* __restrict__ base, const
     m.p = reinterpret_cast<const uint32_t*>(base + d.off - m.sh);
     m.sel = (m.sh + 3u) | ((m.sh + 2u) << 8) | ((m.sh + 1u) << 16) | (m.sh << 24);
     m.len = d.len;
+    m.total = d.total;
     m.nfull = static_cast<uint32_t>(d.len >> 6);
     m.ntb = (static_cast<uint32_t>(d.len) & 63u) < 56u ? 1u : 2u;
     m.out = d.out;
+    m.flags = d.flags;
     return m;
 }
 
@@ -137,7 +140,7 @@ __device__ __forceinline__ void tail_block(const Msg& m, uint32_t tb, uint32_t (
         W[j] = (w & mask) | pad;
     }
     if (tb + 1u == m.ntb) {
-        const uint64_t bits = m.len << 3;
+        const uint64_t bits = m.total << 3;
         W[14] = static_cast<uint32_t>(bits >> 32);
         W[15] = static_cast<uint32_t>(bits);
     }
@@ -192,7 +195,8 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
                                                           uint32_t split, uint32_t n_long, uint32_t cap,
                                                           uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
                                                           uint32_t* __restrict__ queue,
-                                                          uint32_t* __restrict__ census) {
+                                                          uint32_t* __restrict__ census,
+                                                          uint32_t* __restrict__ state) {
     const uint32_t nitems = (n + 63u) >> 6;
     const uint32_t n_short = nitems - n_long;
     const uint32_t lane = threadIdx.x & 63u;
@@ -225,7 +229,14 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
         if (gid < n) {
             const Msg m = msg_setup(base, descs[gid]);
             uint32_t st[8];
-            init_state(st);
+            if (m.flags & kShaResume) {
+                const uint4* s4 = reinterpret_cast<const uint4*>(state + 8ull * m.out);
+                const uint4 s0 = s4[0], s1 = s4[1];
+                st[0] = s0.x; st[1] = s0.y; st[2] = s0.z; st[3] = s0.w;
+                st[4] = s1.x; st[5] = s1.y; st[6] = s1.z; st[7] = s1.w;
+            } else {
+                init_state(st);
+            }
             if (m.nfull) {
                 uint32_t A[16], B[16], xa, xb;
                 load_block(m.p, m.sh, A, xa);
@@ -242,12 +253,18 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
                     if (++k >= m.nfull) break;
                 }
             }
-            for (uint32_t tb = 0; tb < m.ntb; ++tb) {
-                uint32_t W[16];
-                tail_block(m, tb, W);
-                compress(st, W);
+            if (m.flags & kShaPartial) {  // message continues in a later launch
+                uint4* s4 = reinterpret_cast<uint4*>(state + 8ull * m.out);
+                s4[0] = make_uint4(st[0], st[1], st[2], st[3]);
+                s4[1] = make_uint4(st[4], st[5], st[6], st[7]);
+            } else {
+                for (uint32_t tb = 0; tb < m.ntb; ++tb) {
+                    uint32_t W[16];
+                    tail_block(m, tb, W);
+                    compress(st, W);
+                }
+                store_digest(st, m.out, split, out0, out1);
             }
-            store_digest(st, m.out, split, out0, out1);
         }
         if (census && lane == 0u) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
@@ -346,7 +363,7 @@ hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const ui
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
-                         uint32_t* census, hipStream_t s) {
+                         uint32_t* census, hipStream_t s, uint32_t* state) {
     if (n == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
     if (e != hipSuccess) return e;
@@ -357,7 +374,7 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     if (waves > items) waves = items;
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
-                       out1, queue, census);
+                       out1, queue, census, state);
     return hipGetLastError();
 }
 

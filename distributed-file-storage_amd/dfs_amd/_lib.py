@@ -29,6 +29,9 @@ DFS_DEVICE_PTRS = 0x1
 DFS_NO_FILEID = 0x2
 DFS_NO_B64 = 0x4
 DFS_SERIAL = 0x8
+DFS_LAYOUT_FRAG_MAJOR = 0x10
+DFS_SHA_BEGIN = 0x20
+DFS_SHA_FINAL = 0x40
 
 DFS_SPAN_MISSING = (1 << 64) - 1
 
@@ -58,12 +61,14 @@ SIGNATURES = {
     "dfs_b64_decoded_cap": (_u64, [_u64]),
     "dfs_fragment_holders": (_int, [_u32, _u32, _vp]),
     "dfs_sha256_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _u32]),
+    "dfs_sha256_update_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _u32]),
+    "dfs_receive_fragments_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_b64_encode_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _u64, _vp, _u32]),
     "dfs_b64_decode_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]),
     "dfs_upload_batch": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _u32]),
     "dfs_reassemble_verify": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_download_batch": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
-    "dfs_upload_plan_create": (_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
+    "dfs_upload_plan_create": (_int, [_vp, _vp, _u32, _u32, _u32, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
     "dfs_upload_plan_b64_offsets": (_int, [_vp, _vp]),
     "dfs_upload_plan_run": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_upload_plan_destroy": (_int, [_vp]),

@@ -135,6 +135,50 @@ class FragmentEngine:
     def sha256_hex(self, data: bytes) -> str:
         return self.sha256([data])[0].hex()
 
+    def sha256_update(self, parts: Sequence[bytes], state: np.ndarray, begin: bool, final: bool,
+                      total_len: Optional[Sequence[int]] = None) -> Optional[List[bytes]]:
+        """One streaming step (dfs_sha256_update_batch): hash the next part of
+        every message; `state` is an (n, 8) uint32 array updated in place.
+        Returns the digests when final."""
+        buf, spans = _pack(parts)
+        n = len(parts)
+        assert state.shape == (n, 8) and state.dtype == np.uint32 and state.flags.c_contiguous
+        flags = (L.DFS_SHA_BEGIN if begin else 0) | (L.DFS_SHA_FINAL if final else 0)
+        tl = np.array(list(total_len) if total_len is not None else [0] * n, dtype=np.uint64)
+        out = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        check(lib().dfs_sha256_update_batch(self._ctx, _ptr(buf), _ptr(spans), n, _ptr(state), _ptr(tl),
+                                            _ptr(out), flags), "dfs_sha256_update_batch")
+        return [out[i].tobytes() for i in range(n)] if final else None
+
+    def receive_fragments(self, texts: Sequence[bytes]) -> List[Tuple[Optional[bytes], Optional[str]]]:
+        """handleInternalStoreFragments (SN:265-293): per received Base64
+        fragment, (decoded bytes, sha256 hex) or (None, None) where the JDK
+        decoder throws."""
+        buf, spans = _pack(texts)
+        n = len(texts)
+        caps = [lib().dfs_b64_decoded_cap(len(t)) for t in texts]
+        out_off = np.zeros(max(n, 1), dtype=np.uint64)
+        o = 0
+        for i, cp in enumerate(caps):
+            out_off[i] = o
+            o += cp
+        out = np.zeros(max(o, 1), dtype=np.uint8)
+        out_len = np.zeros(max(n, 1), dtype=np.uint64)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        dig = np.zeros((max(n, 1), 32), dtype=np.uint8)
+        rc = lib().dfs_receive_fragments_batch(self._ctx, _ptr(buf), _ptr(spans), n, _ptr(out), _ptr(out_off),
+                                              _ptr(out_len), _ptr(dig), _ptr(status), 0)
+        if rc not in (L.DFS_OK, L.DFS_E_DECODE):
+            check(rc, "dfs_receive_fragments_batch")
+        res = []
+        for i in range(n):
+            if status[i]:
+                res.append((None, None))
+            else:
+                a = int(out_off[i])
+                res.append((out[a:a + int(out_len[i])].tobytes(), dig[i].tobytes().hex()))
+        return res
+
     # -- Base64 (SN:636 encode, SN:281 decode) --------------------------------
     def b64_encode(self, messages: Sequence[bytes]) -> List[bytes]:
         buf, spans = _pack(messages)
@@ -293,18 +337,36 @@ class FragmentEngine:
         return res
 
 
+def download_device(engine: "FragmentEngine", d_b64: int, spans: np.ndarray, nfiles: int, nfrag: int,
+                    file_len: np.ndarray, d_exp_frag: int, d_exp_file: int, d_out: int,
+                    file_off: np.ndarray) -> np.ndarray:
+    """dfs_download_batch on device buffers; returns the per-file status."""
+    spans = np.ascontiguousarray(spans, dtype=np.uint64)
+    file_len = np.ascontiguousarray(file_len, dtype=np.uint64)
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
+    status = np.zeros(max(nfiles, 1), dtype=np.int32)
+    rc = lib().dfs_download_batch(engine.ctx, ctypes.c_void_p(d_b64), _ptr(spans), nfiles, nfrag, _ptr(file_len),
+                                 ctypes.c_void_p(d_exp_frag or None), ctypes.c_void_p(d_exp_file or None),
+                                 ctypes.c_void_p(d_out), _ptr(file_off), _ptr(status), L.DFS_DEVICE_PTRS)
+    if rc not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_DECODE, L.DFS_E_FRAG_MISMATCH, L.DFS_E_CORRUPT):
+        check(rc, "dfs_download_batch")
+    return status[:nfiles]
+
+
 class UploadPlan:
     """dfs_upload_plan over device-resident (torch) buffers — the bench path."""
 
-    def __init__(self, engine: FragmentEngine, spans: np.ndarray, nfrag: int):
+    def __init__(self, engine: FragmentEngine, spans: np.ndarray, nfrag: int, frag_major: bool = False):
         self.engine = engine
         spans = np.ascontiguousarray(spans, dtype=np.uint64)
         self.nfiles = len(spans)
         self.nfrag = nfrag
+        self.frag_major = frag_major
         self._plan = ctypes.c_void_p()
         total = ctypes.c_uint64(0)
-        check(lib().dfs_upload_plan_create(engine.ctx, _ptr(spans), self.nfiles, nfrag, ctypes.byref(self._plan),
-                                           ctypes.byref(total)), "dfs_upload_plan_create")
+        flags = L.DFS_LAYOUT_FRAG_MAJOR if frag_major else 0
+        check(lib().dfs_upload_plan_create(engine.ctx, _ptr(spans), self.nfiles, nfrag, flags,
+                                           ctypes.byref(self._plan), ctypes.byref(total)), "dfs_upload_plan_create")
         self.b64_total = total.value
 
     def b64_offsets(self) -> np.ndarray:

@@ -99,6 +99,21 @@ int dfs_fragment_holders(uint32_t frag, uint32_t nfrag, uint32_t holders[2]);
 int dfs_sha256_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* msgs, uint32_t n,
                      uint8_t* digests, uint32_t flags);
 
+/* Streaming SHA-256 for messages too long to hold at once (the 256 MiB skew
+ * config): each call hashes the next part of every message.
+ *   parts[i]     the bytes of message i in this call (base + off, len)
+ *   state        n*8 uint32 running states (device memory with
+ *                DFS_DEVICE_PTRS, else host); read unless DFS_SHA_BEGIN,
+ *                written unless DFS_SHA_FINAL
+ *   DFS_SHA_FINAL  this is the last part: pad with total_len[i] (host array,
+ *                whole-message length) and write digests[32*i]
+ * Every non-final part must be a multiple of 64 bytes (DFS_E_ARG otherwise).
+ * Concatenated calls give exactly MessageDigest.digest of the whole message. */
+#define DFS_SHA_BEGIN 0x20u
+#define DFS_SHA_FINAL 0x40u
+int dfs_sha256_update_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* parts, uint32_t n,
+                            uint32_t* state, const uint64_t* total_len, uint8_t* digests, uint32_t flags);
+
 /* Base64.getEncoder().encodeToString at SN:636 for `n` messages.  Output i is
  * written at out + out_off[i]; out_off (n+1 entries) is computed by the
  * library as the prefix sum of dfs_b64_encoded_len and returned. */
@@ -113,6 +128,16 @@ int dfs_b64_encode_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* msgs
 int dfs_b64_decode_batch(dfs_ctx* ctx, const char* in, const dfs_span* msgs, uint32_t n,
                          uint8_t* out, const uint64_t* out_off, uint64_t* out_len, int32_t* status,
                          uint32_t flags);
+
+/* The replica receiver, handleInternalStoreFragments (SN:265-293): for each
+ * received fragment, Base64-decode it (SN:281) to out + out_off[i] and
+ * SHA-256 the decoded bytes (SN:282); digests[32*i] is the hash the node
+ * replies with (buildHashResponse, SN:644-655), which the sender compares
+ * with its own (SN:248-257).  status[i] / out_len[i] as dfs_b64_decode_batch;
+ * digests of failed messages are left untouched.  Synchronous. */
+int dfs_receive_fragments_batch(dfs_ctx* ctx, const char* in, const dfs_span* msgs, uint32_t n,
+                                uint8_t* out, const uint64_t* out_off, uint64_t* out_len, uint8_t* digests,
+                                int32_t* status, uint32_t flags);
 
 /* The upload half of handleUpload (SN:118-189) for a batch of files:
  * fileId (SN:127), N-way split (SN:138-157), fragment SHA-256 (SN:159) and
@@ -156,9 +181,15 @@ int dfs_download_batch(dfs_ctx* ctx, const char* b64, const dfs_span* b64_msgs, 
                        int32_t* status, uint32_t flags);
 
 /* ---- prepared upload (descriptor build once, run many; device pointers) --- */
+/* flags: DFS_LAYOUT_FRAG_MAJOR stores the Base64 of fragment i of every file
+ * contiguously ([fragment][file] order) so the bytes bound for one node are
+ * one span (multi-GPU placement exchange); default is [file][fragment]. */
+#define DFS_LAYOUT_FRAG_MAJOR 0x10u
 int dfs_upload_plan_create(dfs_ctx* ctx, const dfs_span* file_spans, uint32_t nfiles, uint32_t nfrag,
-                           dfs_upload_plan** plan, uint64_t* b64_total);
-/* Copy the plan's nfiles*nfrag+1 Base64 offsets to host memory. */
+                           uint32_t flags, dfs_upload_plan** plan, uint64_t* b64_total);
+/* Copy the plan's Base64 offsets to host memory: nfiles*nfrag+1 entries,
+ * entry f*nfrag+i is where fragment i of file f starts (its length is
+ * dfs_b64_encoded_len of the fragment); the last entry is the total. */
 int dfs_upload_plan_b64_offsets(const dfs_upload_plan* plan, uint64_t* b64_off);
 /* Run the plan on device buffers (always asynchronous on the ctx stream). */
 int dfs_upload_plan_run(dfs_ctx* ctx, dfs_upload_plan* plan, const uint8_t* d_files,

@@ -246,6 +246,90 @@ def test_device_plan_and_synth_vs_oracle(engine):
         plan.close()
 
 
+def test_frag_major_plan_and_device_download(engine):
+    """The single-GPU half of bench.py's placement leg: a fragment-major
+    upload plan, then dfs_download_batch on device pointers over the
+    concatenated groups (what exchange_download hands back)."""
+    import torch
+    from dfs_amd import placement as P
+    from dfs_amd.engine import download_device
+    nfiles, S, nfrag = 40, 70001, 5
+    spans = np.array([(f * S, S) for f in range(nfiles)], dtype=np.uint64)
+    files = torch.empty(nfiles * S + 8, dtype=torch.uint8, device="cuda")
+    dfs_amd.synth_fill(engine, files.data_ptr(), spans, 500, O.SYNTH_SEED)
+    plan = dfs_amd.UploadPlan(engine, spans, nfrag, frag_major=True)
+    fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
+    frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
+    b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+    plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
+    torch.cuda.synchronize()
+    offs = plan.b64_offsets()
+    msp = P.frag_major_spans([S] * nfiles, nfrag)
+    assert (msp[:, 0] == offs[:-1]).all()
+    host = files.cpu().numpy()
+    blob = b64.cpu().numpy().tobytes()
+    for f in (0, 17, 39):
+        d = host[f * S:(f + 1) * S].tobytes()
+        for i, (o, ln) in enumerate(O.c_split(S, nfrag)):
+            k = f * nfrag + i
+            assert blob[int(msp[k, 0]):int(msp[k, 0] + msp[k, 1])] == O.c_b64_encode(d[o:o + ln])
+    out = torch.zeros(nfiles * S, dtype=torch.uint8, device="cuda")
+    st = download_device(engine, b64.data_ptr(), msp, nfiles, nfrag, np.full(nfiles, S, np.uint64),
+                         frd.data_ptr(), fd.data_ptr(), out.data_ptr(),
+                         np.arange(nfiles, dtype=np.uint64) * np.uint64(S))
+    assert (st == 0).all()
+    assert torch.equal(out, files[:nfiles * S])
+    plan.close()
+
+
+def test_sha256_update_streaming(engine, golden):
+    """Chunked SHA-256 with carried state == one-shot digest (skew config's
+    streaming path), for several chunkings, message lengths and alignments."""
+    rng = np.random.default_rng(9)
+    msgs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            for n in (0, 1, 63, 64, 65, 191, 192, 1000, 4096, 100003, 262144 + 7)]
+    for chunk in (64, 192, 4096, 65536):
+        state = np.zeros((len(msgs), 8), dtype=np.uint32)
+        nparts = max((len(m) + chunk - 1) // chunk for m in msgs)
+        digests = None
+        for p in range(max(nparts, 1)):
+            final = p == max(nparts, 1) - 1
+            parts = []
+            for m in msgs:
+                a = min(p * chunk, len(m))
+                b = len(m) if final else min((p + 1) * chunk, len(m))
+                parts.append(m[a:b])
+            digests = engine.sha256_update(parts, state, begin=(p == 0), final=final,
+                                           total_len=[len(m) for m in msgs])
+        assert [d.hex() for d in digests] == [hashlib.sha256(m).hexdigest() for m in msgs], chunk
+    # a non-final part that is not a multiple of 64 is rejected
+    with pytest.raises(dfs_amd.DfsError):
+        engine.sha256_update([b"x" * 65], np.zeros((1, 8), np.uint32), begin=True, final=False)
+    # million-'a' KAT in 4 streamed parts
+    kat = golden["sha256_kat"][3]
+    st = np.zeros((1, 8), np.uint32)
+    parts = [b"a" * 262144] * 3 + [b"a" * (1000000 - 3 * 262144)]
+    for i, part in enumerate(parts):
+        d = engine.sha256_update([part], st, begin=(i == 0), final=(i == 3), total_len=[1000000])
+    assert d[0].hex() == kat["digest"]
+
+
+def test_receive_fragments(engine, golden, example_bytes):
+    """handleInternalStoreFragments: decode + hash each received fragment; the
+    digests are what the sender compares with its own (SN:248-257)."""
+    ex = golden["examples"][1]  # id.jpg
+    data = example_bytes[ex["name"]]
+    ups = engine.upload([data], 5)[0]
+    texts = [g.b64 for g in ups.fragments] + [b"Zm9v=", b"", b"Zg"]
+    got = engine.receive_fragments(texts)
+    for g, f, (body, h) in zip(ups.fragments, ex["fragments"], got):
+        assert h == f["sha256"] == g.hash
+        assert body == data[f["offset"]:f["offset"] + f["length"]]
+    assert got[5] == (None, None)
+    assert got[6] == (b"", hashlib.sha256(b"").hexdigest())
+    assert got[7] == (b"f", hashlib.sha256(b"f").hexdigest())
+
+
 def test_profiling_timings(engine):
     engine.set_profiling(True)
     try:
