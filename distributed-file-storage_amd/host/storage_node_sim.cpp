@@ -1,0 +1,235 @@
+// storage_node_sim.cpp — BASELINE config 1 replayed in-process on the GPU path.
+//
+// Five StorageNodes (ids 1..5, TOTAL_NODES = 5, SN:15) share one process;
+// the HTTP hops of the reference (SN:226-259 storeFragments, SN:471-483
+// getFragment, SN:313-350 announce) become direct calls, everything else
+// follows StorageNode.java: node 1 uploads the example files (split, hashes,
+// Base64 and the receivers' decode + hash all run in libdfsgpu.so through
+// FragmentEngine), node 3 then goes down, and nodes 1, 2, 4 and 5 download
+// every file with the reference's fetch order (local, then nodeA = i+1, then
+// nodeB = ((i-1+N)%N)+1, SN:422-440) and verify SHA-256(file) == fileId.
+// Log lines use the reference's formats (SN:125, 128, 136, 160, 167, 209) so
+// config 1's "diff fragment SHA-256s" is a grep + diff.
+//
+// usage: storage_node_sim <file>...   (prints the log to stdout; exit 0 = all
+//        downloads verified bit-exact)
+#include <cstdio>
+#include <fstream>
+#include <iterator>
+#include <map>
+#include <optional>
+#include <set>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "fragment_engine.hpp"
+
+namespace {
+
+constexpr int TOTAL_NODES = 5;  // SN:15
+
+std::string basename_of(const std::string& p) {
+    const size_t s = p.find_last_of('/');
+    return s == std::string::npos ? p : p.substr(s + 1);
+}
+
+// parseJson for /internal/storeFragments bodies (SN:704-753): the same
+// indexOf / split("},{") / strip-quotes procedure.
+std::pair<std::string, std::vector<std::pair<int, std::string>>> parseJson(const std::string& json) {
+    std::string fileId;
+    std::vector<std::pair<int, std::string>> frags;
+    size_t i = json.find("\"fileId\"");
+    if (i != std::string::npos) {
+        size_t colon = json.find(':', i), q1 = json.find('"', colon + 1), q2 = json.find('"', q1 + 1);
+        if (q1 != std::string::npos && q2 != std::string::npos) fileId = json.substr(q1 + 1, q2 - q1 - 1);
+    }
+    size_t k = json.find("\"fragments\"");
+    if (k != std::string::npos) {
+        size_t a = json.find('[', k), b = json.find(']', a);
+        std::string arr = json.substr(a + 1, b - a - 1);
+        size_t pos = 0;
+        while (pos <= arr.size() && !arr.empty()) {
+            size_t nx = arr.find("},{", pos);
+            std::string item = arr.substr(pos, nx == std::string::npos ? std::string::npos : nx - pos);
+            std::string clean;
+            for (char c : item)
+                if (c != '{' && c != '}' && c != '"') clean += c;
+            std::map<std::string, std::string> kv;
+            std::stringstream ss(clean);
+            std::string field;
+            while (std::getline(ss, field, ',')) {
+                size_t c = field.find(':');
+                if (c != std::string::npos) kv[field.substr(0, c)] = field.substr(c + 1);
+            }
+            if (kv.count("index") && kv.count("data")) frags.emplace_back(std::stoi(kv["index"]), kv["data"]);
+            if (nx == std::string::npos) break;
+            pos = nx + 3;
+        }
+    }
+    return {fileId, frags};
+}
+
+struct Node {
+    int id;
+    bool up = true;
+    std::map<std::string, std::map<int, dfs::Bytes>> fragments;  // data/node-<id>/<fileId>/fragments/<i>.frag
+    std::map<std::string, std::string> manifests;                // data/node-<id>/<fileId>/manifest.json
+};
+
+struct Cluster {
+    dfs::FragmentEngine eng;
+    std::vector<Node> nodes;
+    Cluster() {
+        for (int i = 1; i <= TOTAL_NODES; ++i) {
+            nodes.emplace_back();
+            nodes.back().id = i;
+        }
+    }
+    Node& node(int id) { return nodes[id - 1]; }
+
+    // handleInternalStoreFragments (SN:265-293) on node `id`; returns the
+    // {index -> hash} the node replies with (buildHashResponse, SN:644-655).
+    std::map<int, std::string> storeFragments(int id, const std::string& body) {
+        Node& n = node(id);
+        if (!n.up) throw std::runtime_error("Connection refused");
+        auto parsed = parseJson(body);
+        auto got = eng.storeFragments(parsed.second);
+        std::map<int, std::string> resp;
+        for (auto& kv : got) {
+            n.fragments[parsed.first][kv.first] = kv.second.first;  // Files.write(<i>.frag), SN:284-285
+            resp[kv.first] = kv.second.second;
+        }
+        return resp;
+    }
+
+    // handleUpload on node u (SN:118-189).
+    std::string upload(int u, const std::string& name, const dfs::Bytes& file) {
+        std::printf("[%d] Received upload: %zu bytes\n", u, file.size());
+        auto up = eng.upload(file, TOTAL_NODES);
+        const std::string& fileId = up.first;
+        std::printf("[%d] FileId = %s\n", u, fileId.c_str());
+        std::printf("[%d] Original name = %s\n", u, name.c_str());
+        const int u0 = u - 1, my1 = u0, my2 = (u0 + 1) % TOTAL_NODES;
+        for (const auto& f : up.second) {
+            std::printf("[%d] Fragment %d: %zu bytes, hash=%s\n", u, f.index, f.data.size(), f.hash.c_str());
+            if (f.index == my1 || f.index == my2) {
+                node(u).fragments[fileId][f.index] = f.data;
+                std::printf("[%d] Saved fragment %d locally\n", u, f.index);
+            }
+        }
+        // sendFragmentsToPeers (SN:195-224)
+        for (int k = 0; k < TOTAL_NODES; ++k) {
+            if (k == u0) continue;
+            const int f1 = k, f2 = (k + 1) % TOTAL_NODES;
+            bool ok = false;
+            for (int attempt = 1; attempt <= 3 && !ok; ++attempt) {
+                std::printf("[%d] Sending fragments %d and %d to node %d (attempt %d)\n", u, f1, f2, k + 1, attempt);
+                try {
+                    const std::string body = dfs::buildFragmentsJson(fileId, {&up.second[f1], &up.second[f2]});
+                    auto remote = storeFragments(k + 1, body);
+                    ok = true;
+                    for (int fi : {f1, f2}) {  // SN:250-257
+                        if (remote[fi] != up.second[fi].hash) {
+                            std::printf("[%d] Hash mismatch on fragment %d (local=%s, remote=%s)\n", u, fi,
+                                        up.second[fi].hash.c_str(), remote[fi].c_str());
+                            ok = false;
+                        }
+                    }
+                } catch (const std::exception&) {
+                }
+            }
+            if (!ok) {
+                std::printf("[%d] FAILED sending to node %d\n", u, k + 1);
+                return "";  // 500 "Replication failed", SN:174-177
+            }
+        }
+        const std::string manifest = dfs::buildManifestJson(fileId, name, TOTAL_NODES);
+        for (auto& n : nodes) n.manifests[fileId] = manifest;  // save + announce (SN:180-186)
+        std::printf("[%d] Uploaded %s\n", u, name.c_str());
+        return fileId;
+    }
+
+    // handleDownload on node r (SN:399-461): returns the file bytes.
+    dfs::Bytes download(int r, const std::string& fileId, std::string& plan) {
+        std::vector<std::optional<dfs::Bytes>> frags(TOTAL_NODES);
+        plan.clear();
+        for (int i = 0; i < TOTAL_NODES; ++i) {
+            auto& local = node(r).fragments[fileId];
+            std::string src = "missing";
+            if (local.count(i)) {
+                frags[i] = local[i];
+                src = "local";
+            } else {
+                const int cand[2] = {i + 1, ((i - 1 + TOTAL_NODES) % TOTAL_NODES) + 1};  // SN:427-428
+                for (int nd : cand) {
+                    if (nd == r) continue;  // SN:433
+                    Node& peer = node(nd);
+                    if (!peer.up) continue;  // IOException swallowed, SN:439
+                    auto it = peer.fragments[fileId].find(i);
+                    if (it == peer.fragments[fileId].end()) continue;  // 404 -> null
+                    frags[i] = it->second;
+                    src = "node" + std::to_string(nd);
+                    break;
+                }
+            }
+            plan += (i ? "," : "") + src;
+        }
+        return eng.reassembleAndVerify(fileId, frags);  // SN:448-458
+    }
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s <file>...\n", argv[0]);
+        return 2;
+    }
+    try {
+        Cluster c;
+        std::vector<std::pair<std::string, dfs::Bytes>> files;
+        std::vector<std::string> ids;
+        for (int a = 1; a < argc; ++a) {
+            std::ifstream in(argv[a], std::ios::binary);
+            if (!in) throw std::runtime_error(std::string("cannot read ") + argv[a]);
+            dfs::Bytes b((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+            files.emplace_back(basename_of(argv[a]), b);
+            const std::string id = c.upload(1, files.back().first, b);
+            if (id.empty()) return 1;
+            ids.push_back(id);
+        }
+        c.node(3).up = false;  // config 1: node 3 down after the uploads
+        std::printf("[sim] node 3 is down\n");
+        int bad = 0;
+        for (int r : {1, 2, 4, 5}) {
+            for (size_t k = 0; k < files.size(); ++k) {
+                std::string plan;
+                try {
+                    dfs::Bytes got = c.download(r, ids[k], plan);
+                    const bool same = got == files[k].second;
+                    std::printf("[%d] Download %s fileId=%s plan=%s -> %zu bytes %s\n", r, files[k].first.c_str(),
+                                ids[k].c_str(), plan.c_str(), got.size(), same ? "OK" : "MISMATCH");
+                    bad += !same;
+                } catch (const dfs::DownloadError& e) {
+                    std::printf("[%d] Download %s -> 500 %s\n", r, files[k].first.c_str(), e.what());
+                    ++bad;
+                }
+            }
+        }
+        // both holders of fragment 2 (nodes 3 and 2) down -> SN:443-446
+        c.node(2).up = false;
+        std::string plan;
+        try {
+            c.download(1, ids[0], plan);
+            std::printf("[1] Download with nodes 2,3 down -> unexpectedly OK\n");
+            ++bad;
+        } catch (const dfs::DownloadError& e) {
+            std::printf("[1] Download with nodes 2,3 down -> 500 %s\n", e.what());
+        }
+        return bad ? 1 : 0;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "storage_node_sim: %s\n", e.what());
+        return 3;
+    }
+}

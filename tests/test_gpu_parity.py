@@ -4,6 +4,7 @@ Bar: bit-exact digests and bytes (integer/byte work).  Every call goes through
 the C ABI of libdfsgpu.so; the oracle is only the checker.
 """
 import base64
+import os
 import hashlib
 import random
 
@@ -339,3 +340,29 @@ def test_profiling_timings(engine):
         assert t["b64enc"] is not None and t["b64enc"] > 0
     finally:
         engine.set_profiling(False)
+
+
+def test_storage_node_sim_config1(golden):
+    """BASELINE config 1 replayed through the C++ host mirror: 5 nodes, upload
+    examples/* at node 1, node 3 down, download at nodes 1, 2, 4, 5.  The
+    fragment log lines must equal the golden ones and the
+    fetch plans the reference's."""
+    import subprocess
+    from conftest import EXAMPLES, PKG
+    names = [e["name"] for e in golden["examples"]]
+    exe = os.path.join(PKG, "host", "storage_node_sim")
+    r = subprocess.run([exe] + [os.path.join(EXAMPLES, n) for n in names], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = r.stdout.splitlines()
+    frag_lines = [l for l in lines if l.startswith("[1] Fragment ")]
+    assert frag_lines == [l for e in golden["examples"] for l in e["log_lines"]]
+    ids = [l.split("= ")[1] for l in lines if l.startswith("[1] FileId = ")]
+    assert ids == [e["fileId"] for e in golden["examples"]]
+    plans = golden["download_plan_node3_down"]
+    for me in (1, 2, 4, 5):
+        for e in golden["examples"]:
+            want = "[%d] Download %s fileId=%s plan=%s -> %d bytes OK" % (
+                me, e["name"], e["fileId"], ",".join(plans[str(me)]), e["size"])
+            assert want in lines, want
+    assert "[1] Download with nodes 2,3 down -> 500 Could not retrieve fragment 2" in lines
