@@ -34,6 +34,13 @@ __device__ __forceinline__ uint32_t enc4(const uint8_t* __restrict__ lut, uint32
     return c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// PER groups per thread per tile (tile = PER*256 groups); NT bit 0 =
+// non-temporal (streaming) stores, bit 1 = non-temporal loads: this pass
+// never re-reads the Base64 it writes, and its input only via the SHA kernel
+// beside it (which is why loads stay temporal by default).
+template <int PER, int NT>
 __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t* __restrict__ base,
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
@@ -58,8 +65,8 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
         const uint8_t* __restrict__ src = base + jobs[j].src_off;
         uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(out) + jobs[j].dst_off;
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
-        const uint64_t g0 = (t - jobs[j].tile_start) * kEncGroupsPerTile + threadIdx.x;
-        constexpr int kPer = kEncGroupsPerTile / kStreamBlock;
+        const uint64_t g0 = (t - jobs[j].tile_start) * (PER * kStreamBlock) + threadIdx.x;
+        constexpr int kPer = PER;
         // Issue every group's loads first (memory-level parallelism), then
         // encode and store.
         uint4 raw[kPer];
@@ -69,8 +76,19 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
             raw[i] = make_uint4(0u, 0u, 0u, 0u);
             if (g < nfg) {
                 const uint32_t* w = reinterpret_cast<const uint32_t*>(src + 12 * g - sa);
-                if (sa) raw[i] = *reinterpret_cast<const uint4*>(w);
-                else raw[i] = make_uint4(w[0], w[1], w[2], 0u);
+                if (sa) {
+                    if (NT & 2) {
+                        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
+                        raw[i] = make_uint4(v.x, v.y, v.z, v.w);
+                    } else {
+                        raw[i] = *reinterpret_cast<const uint4*>(w);
+                    }
+                } else if (NT & 2) {
+                    raw[i] = make_uint4(__builtin_nontemporal_load(w), __builtin_nontemporal_load(w + 1),
+                                        __builtin_nontemporal_load(w + 2), 0u);
+                } else {
+                    raw[i] = make_uint4(w[0], w[1], w[2], 0u);
+                }
             }
         }
 #pragma unroll
@@ -87,7 +105,12 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
                 const uint32_t g2v = __builtin_amdgcn_perm(u2, u1, 0x0c020304u);
                 const uint32_t g3v = __builtin_amdgcn_perm(0u, u2, 0x0c010203u);
                 const uint4 o = make_uint4(enc4(lut, g0v), enc4(lut, g1v), enc4(lut, g2v), enc4(lut, g3v));
-                *reinterpret_cast<uint4*>(dst + 16 * g) = o;
+                if (NT & 1) {
+                    const u32x4 v = {o.x, o.y, o.z, o.w};
+                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + 16 * g));
+                } else {
+                    *reinterpret_cast<uint4*>(dst + 16 * g) = o;
+                }
             } else if (g == nfg && rem) {
                 // Last partial group: full triples then "==" / "=" padding (RFC 4648 §4).
                 uint32_t* o = reinterpret_cast<uint32_t*>(dst + 16 * g);
@@ -289,10 +312,21 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
 }  // namespace
 
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, char* out,
-                             uint32_t wgs_per_cu, hipStream_t s) {
+                             uint32_t wgs_per_cu, hipStream_t s, int per, int nt) {
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(b64_encode_kernel, dim3(stream_grid(ntiles, wgs_per_cu)), dim3(kStreamBlock), 0, s, base, jobs,
-                       njobs, ntiles, out);
+    const dim3 g(stream_grid(ntiles, wgs_per_cu)), b(kStreamBlock);
+#define DFS_ENC(P, N) hipLaunchKernelGGL((b64_encode_kernel<P, N>), g, b, 0, s, base, jobs, njobs, ntiles, out)
+    switch ((per == 8 ? 4 : 0) | (nt & 3)) {
+        case 0: DFS_ENC(4, 0); break;
+        case 1: DFS_ENC(4, 1); break;
+        case 2: DFS_ENC(4, 2); break;
+        case 3: DFS_ENC(4, 3); break;
+        case 4: DFS_ENC(8, 0); break;
+        case 5: DFS_ENC(8, 1); break;
+        case 6: DFS_ENC(8, 2); break;
+        default: DFS_ENC(8, 3); break;
+    }
+#undef DFS_ENC
     return hipGetLastError();
 }
 

@@ -63,6 +63,8 @@ struct dfs_ctx {
     bool profiling = false;
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
     int b64_wgs = 6;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
+    int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
+    int b64_nt = 1;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
     DevBuf buf[B_COUNT];
@@ -85,6 +87,7 @@ struct dfs_upload_plan {
     StreamJob* d_enc = nullptr;
     uint32_t n_enc = 0;
     uint64_t enc_tiles = 0;
+    int enc_per = 4;  // groups per thread the encode tiles were built for
     std::vector<uint64_t> b64_off;
     uint64_t b64_total = 0;
 };
@@ -263,6 +266,8 @@ int dfs_open(dfs_ctx** out, int device) {
     c->device = device;
     if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
+    if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
+    if (const char* w = std::getenv("DFS_B64_NT")) c->b64_nt = std::atoi(w) & 3;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
@@ -499,7 +504,7 @@ int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, 
     out_off[n] = total;
     if (total > out_cap || (total && !out) || (end && !base)) return DFS_E_ARG;
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kEncGroupsPerTile);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->b64_per) * dfs::kStreamBlock);
     const uint8_t* d_base = base;
     char* d_out = out;
     if (!dev) {
@@ -513,7 +518,8 @@ int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, 
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64ENC, s);
-    HIPC(dfs::launch_b64_encode(d_base, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s));
+    HIPC(dfs::launch_b64_encode(d_base, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s, c->b64_per,
+                                c->b64_nt));
     tm.end(DFS_T_B64ENC, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -659,7 +665,8 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     p->n_all = static_cast<uint32_t>(all.size());
     p->n_frag_only = static_cast<uint32_t>(frag.size());
     p->n_enc = static_cast<uint32_t>(enc.size());
-    p->enc_tiles = finish_jobs(enc, items, dfs::kEncGroupsPerTile);
+    p->enc_per = c->b64_per;
+    p->enc_tiles = finish_jobs(enc, items, static_cast<uint64_t>(p->enc_per) * dfs::kStreamBlock);
     std::vector<ShaDesc> pair;
     std::vector<uint32_t> seq;
     build_pairs(
@@ -757,7 +764,7 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     if (do_b64) {
         tm.begin(DFS_T_B64ENC, sb);
         HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64,
-                                    serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb));
+                                    serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb, p->enc_per, c->b64_nt));
         tm.end(DFS_T_B64ENC, sb);
         if (!serial) {  // join
             HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER + 1], sb));

@@ -59,8 +59,10 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
 // Lane-sequence SHA-256: lane l hashes descs[seq[l] .. seq[l+1]) in order.
 hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const uint32_t* seq, uint32_t nlanes,
                              uint32_t split, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s);
+// Tiles hold per*256 groups (per = 4 or 8, must match the tile count the jobs
+// were built with); nt bit 0 = non-temporal stores, bit 1 = non-temporal loads.
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             char* out, uint32_t wgs_per_cu, hipStream_t s);
+                             char* out, uint32_t wgs_per_cu, hipStream_t s, int per = 4, int nt = 0);
 // Decode: chars of job j at in + src_off decode to out + dst_off.
 // status[id] |= 1 on an IllegalArgumentException case; out_len[id] = bytes.
 // If job.expect != 0 it is the expected decoded length + 1 (download path):

@@ -40,6 +40,34 @@ DEFOP(and_or, "v_and_or_b32 %0, %0, %1, %2")
 DEFOP(pk_add_u16, "v_pk_add_u16 %0, %0, %1")
 DEFOP(bfe, "v_bfe_u32 %0, %0, 6, 6")
 DEFOP(mad_u24, "v_mad_u32_u24 %0, %0, %1, %2")
+DEFOP(lshl, "v_lshlrev_b32_e32 %0, 7, %0")
+DEFOP(and2, "v_and_b32_e32 %0, %0, %1")
+DEFOP(mov, "v_mov_b32_e32 %0, %1")
+
+// 64-bit ops on a register pair (a:a'): one op counts once.
+#define DEFOP64(NAME, ASM)                                                         \
+    struct NAME {                                                                  \
+        static constexpr const char* name = #NAME;                                 \
+        static __device__ __forceinline__ void f(uint32_t& a, uint32_t b, uint32_t c) { \
+            uint64_t x = (static_cast<uint64_t>(b) << 32) | a;                     \
+            asm volatile(ASM : "+v"(x) : "v"(b), "v"(c));                          \
+            a = static_cast<uint32_t>(x);                                          \
+        }                                                                          \
+    };
+DEFOP64(lshr64, "v_lshrrev_b64 %0, 7, %0")
+DEFOP64(lshl64, "v_lshlrev_b64 %0, 7, %0")
+DEFOP64(pk_mov_dup, "v_pk_mov_b32 %0, %0, %0 op_sel:[0,0]")
+DEFOP64(lshl_add64, "v_lshl_add_u64 %0, %0, 2, %0")
+// rotate through a pair: dup (v_pk_mov_b32 low->both) + 64-bit shift = 2
+// instructions per rotate (counted as one op); chain state stays in a pair.
+struct rot64 {
+    static constexpr const char* name = "rot64_dup_shift";
+    static __device__ __forceinline__ void f(uint32_t& a, uint32_t b, uint32_t) {
+        uint64_t x = (static_cast<uint64_t>(b) << 32) | a;
+        asm volatile("v_pk_mov_b32 %0, %0, %0 op_sel:[0,0]\n\tv_lshrrev_b64 %0, 7, %0" : "+v"(x));
+        a = static_cast<uint32_t>(x);
+    }
+};
 
 template <class OP>
 __global__ __launch_bounds__(256) void chains(uint32_t* out, uint32_t seed) {
@@ -105,6 +133,14 @@ int main() {
     run<pk_add_u16>(d, blocks, true);
     run<bfe>(d, blocks, true);
     run<mad_u24>(d, blocks, true);
+    run<lshl>(d, blocks, true);
+    run<and2>(d, blocks, true);
+    run<mov>(d, blocks, true);
+    run<lshr64>(d, blocks, true);
+    run<lshl64>(d, blocks, true);
+    run<pk_mov_dup>(d, blocks, true);
+    run<lshl_add64>(d, blocks, true);
+    run<rot64>(d, blocks, true);
     std::printf("}}\n");
     (void)hipFree(d);
     return 0;
