@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-replicate", action="store_true", help="N>1: skip the placement / degraded-read leg")
     ap.add_argument("--rep-files", type=int, default=8192, help="files per GPU in the placement leg")
     ap.add_argument("--rep-steps", type=int, default=3)
+    ap.add_argument("--no-download", action="store_true", help="skip the download/verify leg")
+    ap.add_argument("--dl-steps", type=int, default=2)
     return ap.parse_args()
 
 
@@ -177,6 +179,53 @@ def replication_leg(args, eng, files, S, N, dev, log):
     result["degraded_download_ok"] = bool(flag.item())
     plan.close()
     return result
+
+
+def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
+    """handleDownload's verify path (SN:399-461) plus north_star's per-fragment
+    check, over this GPU's whole upload: Base64-decode every fragment straight
+    into its file offset (fused gather, SN:448-451), per-fragment SHA-256 vs the
+    upload-time digests, fileId SHA-256 re-verify (SN:454-458) — one
+    dfs_download_batch on device buffers.  Returns a dict for the JSON line."""
+    import numpy as np
+    import torch
+    from dfs_amd.engine import download_device
+    offs = plan.b64_offsets()
+    msp = np.stack([offs[:-1], offs[1:] - offs[:-1]], axis=1).astype(np.uint64)
+    file_len = np.full(F, S, dtype=np.uint64)
+    file_off = np.arange(F, dtype=np.uint64) * np.uint64(S)
+    out = torch.empty(F * S, dtype=torch.uint8, device=dev)
+    reps = max(1, args.dl_steps)
+
+    def once():
+        return download_device(eng, b64.data_ptr(), msp, F, N, file_len, frd.data_ptr(), fd.data_ptr(),
+                               out.data_ptr(), file_off)
+
+    once()
+    torch.cuda.synchronize(dev)
+    eng.set_profiling(True)
+    dec, sha, tot, wall = [], [], [], []
+    ok = True
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        st = once()
+        wall.append(time.perf_counter() - t0)
+        t = eng.timings()
+        dec.append(t["b64dec"]); sha.append(t["sha"]); tot.append(t["total"])
+        ok = ok and bool((st == 0).all())
+    eng.set_profiling(False)
+    ok = ok and bool(torch.equal(out, files[:F * S]))
+    del out
+    dev_ms = float(np.mean(tot))
+    dec_ms = float(np.mean(dec))
+    dec_bytes = int(offs[-1]) + F * S  # Base64 read + bytes written
+    log(f"download: {F} files, device {dev_ms:.1f} ms (decode {dec_ms:.1f}, sha {np.mean(sha):.1f}), ok={ok}")
+    return {"files_per_gpu": F, "device_ms": round(dev_ms, 3), "wall_ms": round(float(np.mean(wall)) * 1e3, 3),
+            "gbps": round(F * S / (dev_ms / 1e3) / 1e9, 2),
+            "decode_ms": round(dec_ms, 3), "decode_gbs": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
+            "decode_frac_hbm": round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "sha_ms": round(float(np.mean(sha)), 3), "ok": ok,
+            "note": "wall_ms includes host-side job planning per call; gbps = file bytes / device time"}
 
 
 def main():
@@ -305,6 +354,11 @@ def main():
                          "ms": round(b64_avg * 1e3, 3), "bytes_per_launch": b64_bytes},
         "verified": ok,
     }
+    if not args.no_download:
+        try:
+            result["download"] = download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log)
+        except Exception as e:
+            result["download"] = {"error": repr(e)[:300]}
     if world > 1 and not args.no_replicate:
         try:
             result["replication"] = replication_leg(args, eng, files, S, N, dev, log)

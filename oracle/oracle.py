@@ -251,3 +251,174 @@ def py_download_plan(my_node: int, n: int, local: Sequence[int], down: Sequence[
             break
         plan.append(src)
     return plan
+
+
+# ---------------------------------------------------------------------------
+# storeFragments wire codec (SN:629-753), restated with java.lang.String
+# semantics: indexOf clamps a negative fromIndex to 0, trim() strips chars
+# <= U+0020 at both ends, split(regex) drops trailing empty strings (and
+# returns [s] when nothing matches), split(regex, 2) keeps them.
+
+class JavaException(Exception):
+    """A RuntimeException the reference would throw (kind = Java class name)."""
+
+    def __init__(self, kind: str):
+        super().__init__(kind)
+        self.kind = kind
+
+
+def j_index_of(s: str, sub: str, start: int = 0) -> int:
+    return s.find(sub, max(start, 0))
+
+
+def j_trim(s: str) -> str:
+    a, b = 0, len(s)
+    while a < b and ord(s[a]) <= 0x20:
+        a += 1
+    while b > a and ord(s[b - 1]) <= 0x20:
+        b -= 1
+    return s[a:b]
+
+
+def j_split(s: str, sep: str, limit: int = 0) -> List[str]:
+    """String.split for a literal separator (the reference's regexes are
+    literal: "\\},\\{", ",", ":")."""
+    if sep not in s:
+        return [s]
+    parts = s.split(sep) if limit <= 0 else s.split(sep, limit - 1)
+    if limit == 0:
+        while parts and parts[-1] == "":
+            parts.pop()
+    return parts
+
+
+def j_parse_int(s: str) -> int:
+    """Integer.parseInt (ASCII digits; NumberFormatException otherwise)."""
+    body = s[1:] if s[:1] in ("-", "+") else s
+    if not body or not all("0" <= c <= "9" for c in body):
+        raise JavaException("NumberFormatException")
+    v = int(s)
+    if v < -2 ** 31 or v > 2 ** 31 - 1:
+        raise JavaException("NumberFormatException")
+    return v
+
+
+def py_parse_json(json: str):
+    """parseJson (SN:704-753): (fileId or None, [{"index": str, "data": str}])."""
+    file_id = None
+    frags = []
+    i = j_index_of(json, '"fileId"')
+    if i != -1:
+        colon = j_index_of(json, ":", i)
+        q1 = j_index_of(json, '"', colon + 1)
+        q2 = j_index_of(json, '"', q1 + 1)
+        if q1 != -1 and q2 != -1:
+            file_id = json[q1 + 1:q2]
+    k = j_index_of(json, '"fragments"')
+    if k != -1:
+        a = j_index_of(json, "[", k)
+        b = j_index_of(json, "]", a)
+        if a != -1 and b != -1:
+            arr = j_trim(json[a + 1:b])
+            if arr:
+                for item in j_split(arr, "},{"):
+                    item = j_trim(item.replace("{", "").replace("}", ""))
+                    frag = {}
+                    for field in j_split(item, ","):
+                        kv = j_split(field, ":", 2)
+                        if len(kv) != 2:
+                            continue
+                        key = j_trim(kv[0]).replace('"', "")
+                        val = j_trim(kv[1]).replace('"', "")
+                        if key in ("index", "data"):
+                            frag[key] = val
+                    if "index" in frag and "data" in frag:
+                        frags.append(frag)
+    return file_id, frags
+
+
+def py_java_hashmap_order(keys: Sequence[int]) -> List[int]:
+    """Iteration order of a java.util.HashMap<Integer, ?> after put(k) for k
+    in `keys` (duplicates keep their first position): buckets ascending
+    under the final table size, insertion order within a bucket."""
+    uniq = []
+    for k in keys:
+        if k not in uniq:
+            uniq.append(k)
+    cap = 16
+    while len(uniq) > cap * 3 // 4:
+        cap *= 2
+
+    def bucket(k):
+        h = k & 0xFFFFFFFF
+        return (h ^ (h >> 16)) & (cap - 1)
+
+    return sorted(uniq, key=lambda k: (bucket(k), uniq.index(k)))
+
+
+def py_build_hash_response(file_id: str, pairs: Sequence[Tuple[int, str]]) -> str:
+    """buildHashResponse (SN:644-655) over the HashMap filled by put(index, hash)."""
+    m = {}
+    for k, h in pairs:
+        m[k] = h
+    items = ['{"index":"%d","hash":"%s"}' % (k, m[k]) for k in py_java_hashmap_order([k for k, _ in pairs])]
+    return '{"fileId":"' + file_id + '","received":[' + ",".join(items) + "]}"
+
+
+def py_parse_response_hashes(json: str) -> dict:
+    """parseResponseHashes (SN:657-701): {index: hash}."""
+    out = {}
+    json = j_trim(json)
+    start = j_index_of(json, '"received"')
+    if start == -1:
+        return out
+    start = j_index_of(json, "[", start)
+    end = j_index_of(json, "]", start)
+    if start == -1 or end == -1:
+        return out
+    if end < start + 1:
+        raise JavaException("StringIndexOutOfBoundsException")
+    arr = j_trim(json[start + 1:end])
+    if not arr:
+        return out
+    for item in j_split(arr, "},{"):
+        item = j_trim(item.replace("{", "").replace("}", "").replace('"', ""))
+        index = None
+        h = None
+        for field in j_split(item, ","):
+            kv = j_split(field, ":", 2)
+            if len(kv) != 2:
+                continue
+            key, value = j_trim(kv[0]), j_trim(kv[1])
+            if key == "index":
+                index = j_parse_int(value)
+            elif key == "hash":
+                h = value
+        if index is not None and h is not None:
+            out[index] = h
+    return out
+
+
+def py_store_fragments(body: bytes):
+    """handleInternalStoreFragments (SN:265-293) on one request body.
+
+    Returns (status, file_id, done, response): status None or the Java
+    exception class that ends the handler; `done` = [(index, data, hash)]
+    for the fragments processed (written to <index>.frag, SN:284-285) before
+    it; `response` = buildHashResponse JSON when status is None.
+    """
+    text = body.decode("utf-8", errors="replace")
+    file_id, frags = py_parse_json(text)
+    if file_id is None:
+        return "NullPointerException", None, [], None  # dataRoot.resolve(null), SN:273
+    done = []
+    for fr in frags:
+        try:
+            index = j_parse_int(fr["index"])
+        except JavaException as e:
+            return e.kind, file_id, done, None
+        data = py_b64_decode_jdk(fr["data"].encode("utf-8"))
+        if data is None:
+            return "IllegalArgumentException", file_id, done, None
+        done.append((index, data, py_sha256_hex(data)))
+    return None, file_id, done, py_build_hash_response(file_id, [(i, h) for i, _, h in done])
