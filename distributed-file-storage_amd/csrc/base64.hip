@@ -36,22 +36,120 @@ __device__ __forceinline__ uint32_t enc4(const uint8_t* __restrict__ lut, uint32
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// 64-entry alphabet as LE words (kAlphaWords) expanded to a 4,096-entry
+// table of character PAIRS: pair[k] = alpha[k >> 6] | alpha[k & 63] << 8, so
+// one 24-bit group is two LDS reads (its high and low 12 bits) and no
+// per-character shifts/masks.  8 KiB per workgroup, built once per
+// (persistent) workgroup.
+__device__ __forceinline__ void build_pair_lut(uint16_t* pair) {
+    const uint8_t* a = reinterpret_cast<const uint8_t*>(kAlphaWords);
+    for (uint32_t k = threadIdx.x; k < 4096u; k += blockDim.x)
+        pair[k] = static_cast<uint16_t>(a[k >> 6] | (static_cast<uint32_t>(a[k & 63u]) << 8));
+}
+
+// x + x on the full-rate adder (the compiler would emit v_lshlrev_b32, a
+// half-rate op on gfx950: tools/valu_peak).
+__device__ __forceinline__ uint32_t dbl(uint32_t x) {
+    uint32_t r;
+    asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// Four ASCII chars (first char in the low byte) of the 24-bit group v:
+// byte addresses 2*(v>>12) and 2*(v&0xfff) into the pair table.
+__device__ __forceinline__ uint32_t enc4_pair(const uint16_t* __restrict__ pair, uint32_t v) {
+    const char* p = reinterpret_cast<const char*>(pair);
+    const uint32_t hi = *reinterpret_cast<const uint16_t*>(p + ((v >> 11) & 0x1ffeu));
+    const uint32_t lo = *reinterpret_cast<const uint16_t*>(p + dbl(v & 0xfffu));
+    return __builtin_amdgcn_perm(lo, hi, 0x05040100u);
+}
+
+// perm selector that yields the big-endian 24-bit group at byte position p
+// of the 16 raw bytes {raw[d], raw[d+1]} (d = p / 4).
+constexpr uint32_t grp_sel(int p) {
+    return static_cast<uint32_t>((p + 2) - 4 * (p / 4)) | (static_cast<uint32_t>((p + 1) - 4 * (p / 4)) << 8) |
+           (static_cast<uint32_t>(p - 4 * (p / 4)) << 16) | (0x0cu << 24);
+}
+template <int P>
+__device__ __forceinline__ uint32_t grp(const uint32_t (&raw)[4]) {
+    constexpr int d = P / 4;
+    return __builtin_amdgcn_perm(d + 1 < 4 ? raw[d + 1 < 4 ? d + 1 : 3] : 0u, raw[d], grp_sel(P));
+}
+
+// One tile of full 12-byte groups whose source starts SA bytes past a dword
+// boundary.  tsrc (dword aligned, = first group - SA) and tdst are uniform;
+// every per-lane address is a constant 32-bit offset from them.
+template <int PER, int NT, bool PAIR, int SA>
+__device__ __forceinline__ void enc_tile(const uint32_t* __restrict__ tsrc, uint8_t* __restrict__ tdst,
+                                         int64_t left, const uint8_t* __restrict__ lut,
+                                         const uint16_t* __restrict__ pair) {
+    uint32_t raw[PER][4];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t lg = threadIdx.x + static_cast<uint32_t>(i) * kStreamBlock;
+        raw[i][0] = raw[i][1] = raw[i][2] = raw[i][3] = 0u;
+        if (static_cast<int64_t>(lg) < left) {
+            const uint32_t* w = tsrc + 3u * lg;
+            if (SA) {
+                u32x4 v;
+                if (NT & 2) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
+                else v = *reinterpret_cast<const u32x4*>(w);
+                raw[i][0] = v.x; raw[i][1] = v.y; raw[i][2] = v.z; raw[i][3] = v.w;
+            } else if (NT & 2) {
+                raw[i][0] = __builtin_nontemporal_load(w);
+                raw[i][1] = __builtin_nontemporal_load(w + 1);
+                raw[i][2] = __builtin_nontemporal_load(w + 2);
+            } else {
+                raw[i][0] = w[0]; raw[i][1] = w[1]; raw[i][2] = w[2];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t lg = threadIdx.x + static_cast<uint32_t>(i) * kStreamBlock;
+        if (static_cast<int64_t>(lg) < left) {
+            uint32_t g[4] = {grp<SA>(raw[i]), grp<SA + 3>(raw[i]), grp<SA + 6>(raw[i]), grp<SA + 9>(raw[i])};
+            u32x4 o;
+            if (PAIR) {
+                o = u32x4{enc4_pair(pair, g[0]), enc4_pair(pair, g[1]), enc4_pair(pair, g[2]), enc4_pair(pair, g[3])};
+            } else {
+                o = u32x4{enc4(lut, g[0]), enc4(lut, g[1]), enc4(lut, g[2]), enc4(lut, g[3])};
+            }
+            u32x4* d = reinterpret_cast<u32x4*>(tdst + 16u * lg);
+            if (NT & 1) __builtin_nontemporal_store(o, d);
+            else *d = o;
+        }
+    }
+}
+
 // PER groups per thread per tile (tile = PER*256 groups); NT bit 0 =
 // non-temporal (streaming) stores, bit 1 = non-temporal loads: this pass
 // never re-reads the Base64 it writes, and its input only via the SHA kernel
-// beside it (which is why loads stay temporal by default).
-template <int PER, int NT>
+// beside it (which is why loads stay temporal by default).  PAIR selects the
+// 12-bit pair table (2 LDS reads + 5 VALU per group) over the 6-bit
+// alphabet (4 LDS reads + ~10 VALU per group).
+template <int PER, int NT, bool PAIR>
 __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t* __restrict__ base,
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
-                                                                  char* __restrict__ out) {
+                                                                  char* __restrict__ out, uint32_t prio) {
     // Memory-bound waves issue first: beside the VALU-bound SHA kernel they
     // need few issue slots but must keep their loads in flight.
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ uint32_t lut_words[16];
-    if (threadIdx.x < 16) lut_words[threadIdx.x] = kAlphaWords[threadIdx.x];
+    switch (prio) {  // s_setprio takes an immediate
+        case 0: break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+    __shared__ uint32_t lut_words[PAIR ? 2048 : 16];
+    if (PAIR) {
+        build_pair_lut(reinterpret_cast<uint16_t*>(lut_words));
+    } else if (threadIdx.x < 16) {
+        lut_words[threadIdx.x] = kAlphaWords[threadIdx.x];
+    }
     __syncthreads();
     const uint8_t* lut = reinterpret_cast<const uint8_t*>(lut_words);
+    const uint16_t* pair = reinterpret_cast<const uint16_t*>(lut_words);
 
     uint64_t t0, t1;
     tile_range(ntiles, t0, t1);
@@ -65,66 +163,29 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
         const uint8_t* __restrict__ src = base + jobs[j].src_off;
         uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(out) + jobs[j].dst_off;
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
-        const uint64_t g0 = (t - jobs[j].tile_start) * (PER * kStreamBlock) + threadIdx.x;
-        constexpr int kPer = PER;
-        // Issue every group's loads first (memory-level parallelism), then
-        // encode and store.
-        uint4 raw[kPer];
-#pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-            const uint64_t g = g0 + static_cast<uint64_t>(i) * kStreamBlock;
-            raw[i] = make_uint4(0u, 0u, 0u, 0u);
-            if (g < nfg) {
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + 12 * g - sa);
-                if (sa) {
-                    if (NT & 2) {
-                        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
-                        raw[i] = make_uint4(v.x, v.y, v.z, v.w);
-                    } else {
-                        raw[i] = *reinterpret_cast<const uint4*>(w);
-                    }
-                } else if (NT & 2) {
-                    raw[i] = make_uint4(__builtin_nontemporal_load(w), __builtin_nontemporal_load(w + 1),
-                                        __builtin_nontemporal_load(w + 2), 0u);
-                } else {
-                    raw[i] = make_uint4(w[0], w[1], w[2], 0u);
-                }
-            }
+        const uint64_t tg = (t - jobs[j].tile_start) * (PER * kStreamBlock);  // first group of the tile
+        const int64_t left = static_cast<int64_t>(nfg) - static_cast<int64_t>(tg);
+        const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(src + 12 * tg - sa);
+        uint8_t* tdst = dst + 16 * tg;
+        switch (sa) {  // wave-uniform
+            case 0: enc_tile<PER, NT, PAIR, 0>(tsrc, tdst, left, lut, pair); break;
+            case 1: enc_tile<PER, NT, PAIR, 1>(tsrc, tdst, left, lut, pair); break;
+            case 2: enc_tile<PER, NT, PAIR, 2>(tsrc, tdst, left, lut, pair); break;
+            default: enc_tile<PER, NT, PAIR, 3>(tsrc, tdst, left, lut, pair); break;
         }
-#pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-            const uint64_t g = g0 + static_cast<uint64_t>(i) * kStreamBlock;
-            if (g < nfg) {
-                const uint4 v = raw[i];
-                const uint32_t u0 = align_bytes(v.y, v.x, sa);
-                const uint32_t u1 = align_bytes(v.z, v.y, sa);
-                const uint32_t u2 = align_bytes(v.w, v.z, sa);
-                // Big-endian 24-bit groups: bytes (0,1,2) (3,4,5) (6,7,8) (9,10,11).
-                const uint32_t g0v = __builtin_amdgcn_perm(0u, u0, 0x0c000102u);
-                const uint32_t g1v = __builtin_amdgcn_perm(u1, u0, 0x0c030405u);
-                const uint32_t g2v = __builtin_amdgcn_perm(u2, u1, 0x0c020304u);
-                const uint32_t g3v = __builtin_amdgcn_perm(0u, u2, 0x0c010203u);
-                const uint4 o = make_uint4(enc4(lut, g0v), enc4(lut, g1v), enc4(lut, g2v), enc4(lut, g3v));
-                if (NT & 1) {
-                    const u32x4 v = {o.x, o.y, o.z, o.w};
-                    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + 16 * g));
-                } else {
-                    *reinterpret_cast<uint4*>(dst + 16 * g) = o;
-                }
-            } else if (g == nfg && rem) {
-                // Last partial group: full triples then "==" / "=" padding (RFC 4648 §4).
-                uint32_t* o = reinterpret_cast<uint32_t*>(dst + 16 * g);
-                const uint8_t* s = src + 12 * g;
-                for (uint32_t k = 0; k < rem; k += 3) {
-                    const uint32_t n = rem - k < 3 ? rem - k : 3;
-                    uint32_t v = static_cast<uint32_t>(s[k]) << 16;
-                    if (n > 1) v |= static_cast<uint32_t>(s[k + 1]) << 8;
-                    if (n > 2) v |= s[k + 2];
-                    uint32_t wv = enc4(lut, v);
-                    if (n == 1) wv = (wv & 0x0000ffffu) | 0x3d3d0000u;  // "xx=="
-                    else if (n == 2) wv = (wv & 0x00ffffffu) | 0x3d000000u;  // "xxx="
-                    o[k / 3] = wv;
-                }
+        // Last partial group: full triples then "==" / "=" padding (RFC 4648 §4).
+        if (rem && left >= 0 && left < PER * kStreamBlock && threadIdx.x == static_cast<uint32_t>(left) % kStreamBlock) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(dst + 16 * nfg);
+            const uint8_t* s = src + 12 * nfg;
+            for (uint32_t k = 0; k < rem; k += 3) {
+                const uint32_t n = rem - k < 3 ? rem - k : 3;
+                uint32_t v = static_cast<uint32_t>(s[k]) << 16;
+                if (n > 1) v |= static_cast<uint32_t>(s[k + 1]) << 8;
+                if (n > 2) v |= s[k + 2];
+                uint32_t wv = PAIR ? enc4_pair(pair, v) : enc4(lut, v);
+                if (n == 1) wv = (wv & 0x0000ffffu) | 0x3d3d0000u;  // "xx=="
+                else if (n == 2) wv = (wv & 0x00ffffffu) | 0x3d000000u;  // "xxx="
+                o[k / 3] = wv;
             }
         }
     }
@@ -312,20 +373,23 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
 }  // namespace
 
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, char* out,
-                             uint32_t wgs_per_cu, hipStream_t s, int per, int nt) {
+                             uint32_t wgs_per_cu, hipStream_t s, int per, int nt, bool pair, uint32_t prio) {
     if (ntiles == 0) return hipSuccess;
     const dim3 g(stream_grid(ntiles, wgs_per_cu)), b(kStreamBlock);
-#define DFS_ENC(P, N) hipLaunchKernelGGL((b64_encode_kernel<P, N>), g, b, 0, s, base, jobs, njobs, ntiles, out)
-    switch ((per == 8 ? 4 : 0) | (nt & 3)) {
-        case 0: DFS_ENC(4, 0); break;
-        case 1: DFS_ENC(4, 1); break;
-        case 2: DFS_ENC(4, 2); break;
-        case 3: DFS_ENC(4, 3); break;
-        case 4: DFS_ENC(8, 0); break;
-        case 5: DFS_ENC(8, 1); break;
-        case 6: DFS_ENC(8, 2); break;
-        default: DFS_ENC(8, 3); break;
+#define DFS_ENC(P, N, L) hipLaunchKernelGGL((b64_encode_kernel<P, N, L>), g, b, 0, s, base, jobs, njobs, ntiles, out, prio)
+#define DFS_ENC_NT(P, L)                   \
+    switch (nt & 3) {                      \
+        case 0: DFS_ENC(P, 0, L); break;   \
+        case 1: DFS_ENC(P, 1, L); break;   \
+        case 2: DFS_ENC(P, 2, L); break;   \
+        default: DFS_ENC(P, 3, L); break;  \
     }
+    if (per == 8) {
+        if (pair) { DFS_ENC_NT(8, true) } else { DFS_ENC_NT(8, false) }
+    } else {
+        if (pair) { DFS_ENC_NT(4, true) } else { DFS_ENC_NT(4, false) }
+    }
+#undef DFS_ENC_NT
 #undef DFS_ENC
     return hipGetLastError();
 }

@@ -62,9 +62,12 @@ struct dfs_ctx {
     hipStream_t user = nullptr;  // borrowed (dfs_set_stream)
     bool profiling = false;
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
+    uint32_t sha_rot = 1;        // rotate short-item issue priority (DFS_SHA_ROT=0 disables)
     int b64_wgs = 6;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
     int b64_nt = 1;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
+    bool b64_pair = true;        // 12-bit pair table (DFS_B64_LUT=12) vs 6-bit alphabet (=6)
+    uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
     DevBuf buf[B_COUNT];
@@ -265,9 +268,12 @@ int dfs_open(dfs_ctx** out, int device) {
     if (!c) return DFS_E_NOMEM;
     c->device = device;
     if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = std::max(1, std::min(8, std::atoi(w)));
+    if (const char* w = std::getenv("DFS_SHA_ROT")) c->sha_rot = std::atoi(w) ? 1u : 0u;
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
     if (const char* w = std::getenv("DFS_B64_NT")) c->b64_nt = std::atoi(w) & 3;
+    if (const char* w = std::getenv("DFS_B64_LUT")) c->b64_pair = std::atoi(w) != 6;
+    if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
@@ -373,7 +379,7 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
-                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, nullptr, c->sha_rot));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -422,7 +428,7 @@ int dfs_sha256_update_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* par
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
-                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, d_state));
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, d_state, c->sha_rot));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -519,7 +525,7 @@ int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, 
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64ENC, s);
     HIPC(dfs::launch_b64_encode(d_base, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s, c->b64_per,
-                                c->b64_nt));
+                                c->b64_nt, c->b64_pair));
     tm.end(DFS_T_B64ENC, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -755,7 +761,7 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
                                     s));
     } else if (do_fileid) {
         HIPC(dfs::launch_sha256(d_files, p->d_all, p->n_all, p->nfiles, p->prio_all, d_fd, d_frd, p->d_queue,
-                                c->sha_wps, census, s));
+                                c->sha_wps, census, s, nullptr, c->sha_rot));
     } else {
         HIPC(dfs::launch_sha256(d_files, p->d_frag, p->n_frag_only, p->nfiles, p->prio_frag, d_fd, d_frd,
                                 p->d_queue, c->sha_wps, census, s));
@@ -764,7 +770,8 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     if (do_b64) {
         tm.begin(DFS_T_B64ENC, sb);
         HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64,
-                                    serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb, p->enc_per, c->b64_nt));
+                                    serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb, p->enc_per, c->b64_nt,
+                                    c->b64_pair, c->b64_prio));
         tm.end(DFS_T_B64ENC, sb);
         if (!serial) {  // join
             HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER + 1], sb));
@@ -918,7 +925,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
-                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
+                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, nullptr, c->sha_rot));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<uint8_t> dig(32ull * nfiles);
@@ -1038,7 +1045,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
         HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
                                 static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig,
-                                c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
+                                c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, nullptr, c->sha_rot));
     }
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);

@@ -55,14 +55,17 @@ inline uint64_t enc_tiles(uint64_t len) {
 // on each of the 1024 SIMDs (fewer for small batches).
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
-                         int waves_per_simd, uint32_t* census, hipStream_t s, uint32_t* state = nullptr);
+                         int waves_per_simd, uint32_t* census, hipStream_t s, uint32_t* state = nullptr,
+                         uint32_t rot = 1);
 // Lane-sequence SHA-256: lane l hashes descs[seq[l] .. seq[l+1]) in order.
 hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const uint32_t* seq, uint32_t nlanes,
                              uint32_t split, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s);
 // Tiles hold per*256 groups (per = 4 or 8, must match the tile count the jobs
-// were built with); nt bit 0 = non-temporal stores, bit 1 = non-temporal loads.
+// were built with); nt bit 0 = non-temporal stores, bit 1 = non-temporal loads;
+// pair = 12-bit character-pair LDS table (else the 6-bit alphabet).
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             char* out, uint32_t wgs_per_cu, hipStream_t s, int per = 4, int nt = 0);
+                             char* out, uint32_t wgs_per_cu, hipStream_t s, int per = 4, int nt = 0,
+                             bool pair = true, uint32_t prio = 3);
 // Decode: chars of job j at in + src_off decode to out + dst_off.
 // status[id] |= 1 on an IllegalArgumentException case; out_len[id] = bytes.
 // If job.expect != 0 it is the expected decoded length + 1 (download path):

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
                                                           uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
                                                           uint32_t* __restrict__ queue,
                                                           uint32_t* __restrict__ census,
-                                                          uint32_t* __restrict__ state) {
+                                                          uint32_t* __restrict__ state, uint32_t rot) {
     const uint32_t nitems = (n + 63u) >> 6;
     const uint32_t n_short = nitems - n_long;
     const uint32_t lane = threadIdx.x & 63u;
@@ -237,6 +237,14 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
             } else {
                 init_state(st);
             }
+            // Short items rotate their issue priority (0/1, flipped every
+            // two blocks): the SIMD arbiter breaks priority ties by wave
+            // age, so without this the oldest short wave of a SIMD runs
+            // ~2x faster than the youngest and the SIMD ends the kernel
+            // with one wave left (tools/census.py).  Flipping on progress
+            // is self-balancing: a wave that ran ahead spends less time at
+            // the higher priority.
+            const bool flip = rot && item >= n_long;
             if (m.nfull) {
                 uint32_t A[16], B[16], xa, xb;
                 load_block(m.p, m.sh, A, xa);
@@ -251,6 +259,10 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
                     to_be(B, xb, m.sel);
                     compress(st, B);
                     if (++k >= m.nfull) break;
+                    if (flip) {
+                        if (k & 2u) __builtin_amdgcn_s_setprio(1);
+                        else __builtin_amdgcn_s_setprio(0);
+                    }
                 }
             }
             if (m.flags & kShaPartial) {  // message continues in a later launch
@@ -363,7 +375,7 @@ hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const ui
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
-                         uint32_t* census, hipStream_t s, uint32_t* state) {
+                         uint32_t* census, hipStream_t s, uint32_t* state, uint32_t rot) {
     if (n == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
     if (e != hipSuccess) return e;
@@ -374,7 +386,7 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     if (waves > items) waves = items;
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
-                       out1, queue, census, state);
+                       out1, queue, census, state, rot);
     return hipGetLastError();
 }
 
