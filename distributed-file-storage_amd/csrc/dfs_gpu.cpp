@@ -62,8 +62,8 @@ struct dfs_ctx {
     hipStream_t user = nullptr;  // borrowed (dfs_set_stream)
     bool profiling = false;
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
-    uint32_t sha_rot = 1;        // rotate short-item issue priority (DFS_SHA_ROT=0 disables)
-    int b64_wgs = 6;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
+    int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels (DFS_UPLOAD_MODE)
+    int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
     int b64_nt = 1;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
     bool b64_pair = true;        // 12-bit pair table (DFS_B64_LUT=12) vs 6-bit alphabet (=6)
@@ -83,10 +83,6 @@ struct dfs_upload_plan {
     uint32_t prio_all = 0, prio_frag = 0;
     ShaDesc* d_all = nullptr;
     ShaDesc* d_frag = nullptr;
-    // Paired lane sequences (fileId lane + fragment-sequence lane per file).
-    ShaDesc* d_pair = nullptr;
-    uint32_t* d_seq = nullptr;
-    uint32_t n_seq_lanes = 0;
     StreamJob* d_enc = nullptr;
     uint32_t n_enc = 0;
     uint64_t enc_tiles = 0;
@@ -124,7 +120,7 @@ void split(uint64_t S, uint32_t N, uint64_t* off, uint64_t* len) {
 uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
 
 // A whole message (not resumed): len bytes at off, digest slot out.
-ShaDesc msg(uint64_t off, uint64_t len, uint64_t out) { return ShaDesc{off, len, len, static_cast<uint32_t>(out), 0}; }
+ShaDesc msg(uint64_t off, uint64_t len, uint64_t out) { return ShaDesc{off, len, len, static_cast<uint32_t>(out), 0, 0}; }
 
 // Sort SHA lanes longest-first (uniform waves) and count the lanes that
 // carry the long chains: those waves get issue priority in the kernel.
@@ -135,45 +131,6 @@ uint32_t sort_lanes(std::vector<ShaDesc>& d) {
     uint32_t n = 0;
     while (n < d.size() && d[n].len >= 2 * med + 64) ++n;
     return (n + 63) & ~63u;
-}
-
-// Paired lane sequences for files whose fileId and fragments are all hashed
-// (sha256_seq): per wave of 64 lanes, lanes 0..31 hash the whole files
-// f0..f0+31 and lanes 32..63 hash the same files' fragments one after the
-// other, so the two lanes of a file walk its bytes in lockstep.  `file_msg`
-// and `frag_msg(f, i)` give the ShaDesc of a file and of its fragment i.
-template <class FileFn, class FragFn>
-void build_pairs(uint32_t nfiles, uint32_t nfrag, FileFn file_msg, FragFn frag_msg, std::vector<ShaDesc>& descs,
-                 std::vector<uint32_t>& seq) {
-    descs.clear();
-    seq.clear();
-    const uint32_t waves = (nfiles + 31) / 32;
-    descs.reserve(static_cast<size_t>(nfiles) * (nfrag + 1));
-    seq.reserve(64ull * waves + 1);
-    for (uint32_t w = 0; w < waves; ++w) {
-        for (uint32_t l = 0; l < 32; ++l) {  // whole-file lanes
-            const uint32_t f = 32 * w + l;
-            seq.push_back(static_cast<uint32_t>(descs.size()));
-            if (f < nfiles) descs.push_back(file_msg(f));
-        }
-        for (uint32_t l = 0; l < 32; ++l) {  // fragment-sequence lanes
-            const uint32_t f = 32 * w + l;
-            seq.push_back(static_cast<uint32_t>(descs.size()));
-            if (f < nfiles)
-                for (uint32_t i = 0; i < nfrag; ++i) descs.push_back(frag_msg(f, i));
-        }
-    }
-    seq.push_back(static_cast<uint32_t>(descs.size()));
-}
-
-// Lane layout for the upload / download SHA work.  Default: one message per
-// lane, persistent sha256_lanes (measured 80 ms vs 129 ms for the paired
-// layout on config 2: the pairs leave only 2 waves per SIMD, too few to hide
-// the VALU dependency latency of the SHA rounds, although they halve the HBM
-// reads).  DFS_SHA_MODE=pairs selects sha256_seq for experiments.
-bool use_pairs() {
-    const char* m = std::getenv("DFS_SHA_MODE");
-    return m && std::strcmp(m, "pairs") == 0;
 }
 
 // Fill tile_start prefix for `items` work items per job; append sentinel.
@@ -268,7 +225,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (!c) return DFS_E_NOMEM;
     c->device = device;
     if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = std::max(1, std::min(8, std::atoi(w)));
-    if (const char* w = std::getenv("DFS_SHA_ROT")) c->sha_rot = std::atoi(w) ? 1u : 0u;
+    if (const char* w = std::getenv("DFS_UPLOAD_MODE")) c->upload_mode = std::strcmp(w, "fused") == 0 ? 0 : 1;
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
     if (const char* w = std::getenv("DFS_B64_NT")) c->b64_nt = std::atoi(w) & 3;
@@ -379,7 +336,7 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
-                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, nullptr, c->sha_rot));
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -428,7 +385,7 @@ int dfs_sha256_update_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* par
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
-                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, d_state, c->sha_rot));
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, d_state));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -666,6 +623,14 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     }
     p->b64_off[nf] = total;
     p->b64_total = total;
+    // Fragment lanes carry their Base64 offset: the fused upload encodes in
+    // the SHA pass (kShaB64 is ignored when the kernel gets no output).
+    for (std::vector<ShaDesc>* v : {&all, &frag})
+        for (ShaDesc& d : *v)
+            if (d.out >= nfiles) {
+                d.b64 = p->b64_off[d.out - nfiles];
+                d.flags |= dfs::kShaB64;
+            }
     p->prio_all = sort_lanes(all);
     p->prio_frag = sort_lanes(frag);
     p->n_all = static_cast<uint32_t>(all.size());
@@ -673,23 +638,7 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     p->n_enc = static_cast<uint32_t>(enc.size());
     p->enc_per = c->b64_per;
     p->enc_tiles = finish_jobs(enc, items, static_cast<uint64_t>(p->enc_per) * dfs::kStreamBlock);
-    std::vector<ShaDesc> pair;
-    std::vector<uint32_t> seq;
-    build_pairs(
-        nfiles, nfrag, [&](uint32_t f) { return msg(files[f].off, files[f].len, f); },
-        [&](uint32_t f, uint32_t i) {
-            const uint64_t base = files[f].len / nfrag, rem = files[f].len % nfrag;
-            const uint64_t o = i * base + (i < rem ? i : rem);
-            return msg(files[f].off + o, base + (i < rem ? 1 : 0), nfiles + static_cast<uint64_t>(f) * nfrag + i);
-        },
-        pair, seq);
-    p->n_seq_lanes = static_cast<uint32_t>(seq.size() - 1);
     hipError_t e = hipMalloc(&p->d_queue, dfs::kShaQueueBytes);
-    if (e == hipSuccess) e = hipMalloc(&p->d_pair, std::max<size_t>(pair.size(), 1) * sizeof(ShaDesc));
-    if (e == hipSuccess) e = hipMalloc(&p->d_seq, seq.size() * sizeof(uint32_t));
-    if (e == hipSuccess && !pair.empty())
-        e = hipMemcpy(p->d_pair, pair.data(), pair.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(p->d_seq, seq.data(), seq.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_all, std::max<size_t>(all.size(), 1) * sizeof(ShaDesc));
     if (e == hipSuccess) e = hipMalloc(&p->d_frag, std::max<size_t>(frag.size(), 1) * sizeof(ShaDesc));
     if (e == hipSuccess) e = hipMalloc(&p->d_enc, enc.size() * sizeof(StreamJob));
@@ -718,8 +667,6 @@ int dfs_upload_plan_destroy(dfs_upload_plan* p) {
     if (!p) return DFS_E_ARG;
     (void)hipSetDevice(p->device);
     if (p->d_queue) (void)hipFree(p->d_queue);
-    if (p->d_pair) (void)hipFree(p->d_pair);
-    if (p->d_seq) (void)hipFree(p->d_seq);
     if (p->d_all) (void)hipFree(p->d_all);
     if (p->d_frag) (void)hipFree(p->d_frag);
     if (p->d_enc) (void)hipFree(p->d_enc);
@@ -733,41 +680,51 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     const bool do_fileid = !(flags & DFS_NO_FILEID);
     const bool do_b64 = !(flags & DFS_NO_B64) && p->n_enc;
     const bool serial = flags & DFS_SERIAL;
+    const bool fused = do_b64 && c->upload_mode == 0 && !serial;
     if (!d_frd || (do_fileid && !d_fd) || (do_b64 && !d_b64)) return DFS_E_ARG;
     if (do_b64 && (reinterpret_cast<uintptr_t>(d_b64) & 3u)) return DFS_E_ARG;
     hipStream_t s = c->stream();
+    if (flags & DFS_B64_ONLY) {  // the HBM-bound encode pass alone
+        if (!do_b64) return DFS_OK;
+        Timer tb(c);
+        tb.begin(DFS_T_TOTAL, s);
+        tb.begin(DFS_T_B64ENC, s);
+        HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64, 8u, s, p->enc_per,
+                                    c->b64_nt, c->b64_pair, c->b64_prio));
+        tb.end(DFS_T_B64ENC, s);
+        tb.end(DFS_T_TOTAL, s);
+        return DFS_OK;
+    }
     hipStream_t sb = serial ? s : c->aux;
     Timer tm(c);
     // Experiment hook: DFS_SHA_CENSUS=<path> dumps {hw_id, xcc_id, t0, t1} per
     // SHA work item (s_memrealtime, 100 MHz) after the call.
     const char* census_path = std::getenv("DFS_SHA_CENSUS");
     uint32_t* census = nullptr;
-    const bool pairs = do_fileid && use_pairs();
-    const uint32_t n_items = pairs ? (p->n_seq_lanes + 63u) / 64u : ((do_fileid ? p->n_all : p->n_frag_only) + 63u) / 64u;
+    const uint32_t n_items = ((do_fileid ? p->n_all : p->n_frag_only) + 63u) / 64u;
     if (census_path) {
         HIPC(c->buf[B_OUTLEN].ensure(16ull * n_items));
         census = c->buf[B_OUTLEN].as<uint32_t>();
         HIPC(hipMemsetAsync(census, 0, 16ull * n_items, s));
     }
+    const bool two = do_b64 && !fused;  // separate Base64 encode kernel
     tm.begin(DFS_T_TOTAL, s);
-    if (do_b64 && !serial) {  // fork: Base64 on the aux stream beside SHA
+    if (two && !serial) {  // fork: Base64 on the aux stream beside SHA
         HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER], s));
         HIPC(hipStreamWaitEvent(sb, c->ev[2 * DFS_T_GATHER], 0));
     }
+    // Fused: the fragment lanes write the Base64 too (kShaB64, sha256.hip).
+    char* fb64 = fused ? d_b64 : nullptr;
     tm.begin(DFS_T_SHA, s);
-    if (pairs) {
-        // out index < nfiles -> file digest, else fragment digest (split = nfiles)
-        HIPC(dfs::launch_sha256_seq(d_files, p->d_pair, p->d_seq, p->n_seq_lanes, p->nfiles, d_fd, d_frd, census,
-                                    s));
-    } else if (do_fileid) {
+    if (do_fileid) {
         HIPC(dfs::launch_sha256(d_files, p->d_all, p->n_all, p->nfiles, p->prio_all, d_fd, d_frd, p->d_queue,
-                                c->sha_wps, census, s, nullptr, c->sha_rot));
+                                c->sha_wps, census, s, nullptr, fb64));
     } else {
         HIPC(dfs::launch_sha256(d_files, p->d_frag, p->n_frag_only, p->nfiles, p->prio_frag, d_fd, d_frd,
-                                p->d_queue, c->sha_wps, census, s));
+                                p->d_queue, c->sha_wps, census, s, nullptr, fb64));
     }
     tm.end(DFS_T_SHA, s);
-    if (do_b64) {
+    if (two) {
         tm.begin(DFS_T_B64ENC, sb);
         HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64,
                                     serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb, p->enc_per, c->b64_nt,
@@ -925,7 +882,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
-                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, nullptr, c->sha_rot));
+                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<uint8_t> dig(32ull * nfiles);
@@ -998,35 +955,9 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
     const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecChunksPerTile);
-    // SHA lanes: paired (whole-file lane + fragment-sequence lane per file,
-    // sha256_seq) or one message per lane (persistent sha256_lanes).
-    const bool pairs = use_pairs();
-    std::vector<uint32_t> seq;
-    uint32_t prio = 0;
-    if (pairs) {
-        std::vector<uint32_t> valid;
-        for (uint32_t f = 0; f < nfiles; ++f)
-            if (status[f] == DFS_OK) valid.push_back(f);
-        build_pairs(
-            static_cast<uint32_t>(valid.size()), nfrag,
-            [&](uint32_t v) {
-                const uint32_t f = valid[v];
-                return msg(file_off[f], file_len[f], nf + f);
-            },
-            [&](uint32_t v, uint32_t i) {
-                const uint32_t f = valid[v];
-                const uint64_t b = file_len[f] / nfrag, rem = file_len[f] % nfrag;
-                const uint64_t o = i * b + (i < rem ? i : rem);
-                return msg(file_off[f] + o, b + (i < rem ? 1 : 0), static_cast<uint64_t>(f) * nfrag + i);
-            },
-            sha, seq);
-    } else {
-        prio = sort_lanes(sha);
-    }
+    const uint32_t prio = sort_lanes(sha);  // one message per lane, persistent sha256_lanes
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
-    if (pairs)
-        if (int rc = put(c, B_JOBS2, seq.data(), seq.size() * sizeof(uint32_t), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * nf));
     HIPC(c->buf[B_DIG0].ensure(32ull * (nf + nfiles)));
     HIPC(hipMemsetAsync(c->buf[B_STATUS].p, 0, 4ull * nf, s));
@@ -1037,16 +968,10 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
                                 c->buf[B_STATUS].as<int32_t>(), nullptr, s));
     tm.end(DFS_T_B64DEC, s);
     tm.begin(DFS_T_SHA, s);
-    if (pairs) {
-        HIPC(dfs::launch_sha256_seq(d_out, c->buf[B_DESC].as<ShaDesc>(), c->buf[B_JOBS2].as<uint32_t>(),
-                                    static_cast<uint32_t>(seq.size() - 1), static_cast<uint32_t>(nf + nfiles), d_dig,
-                                    d_dig, nullptr, s));
-    } else {
-        HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
-        HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
-                                static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig,
-                                c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, nullptr, c->sha_rot));
-    }
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
+                            static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(),
+                            c->sha_wps, nullptr, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(nf);

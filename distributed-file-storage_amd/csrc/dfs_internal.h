@@ -14,7 +14,8 @@ struct ShaDesc {
     uint64_t len;    // bytes hashed by this lane in this launch
     uint64_t total;  // whole-message length (the padding's bit count); = len unless resumed
     uint32_t out;
-    uint32_t flags;  // kShaResume / kShaPartial
+    uint32_t flags;  // kShaResume / kShaPartial / kShaB64
+    uint64_t b64;    // kShaB64: output offset of this fragment's Base64 (dword aligned)
 };
 // Streaming (SHA-256 update across launches, e.g. the 256 MiB skew config):
 // kShaResume: start from the 8-word state in state[8*out] instead of H0;
@@ -22,6 +23,9 @@ struct ShaDesc {
 // running state to state[8*out] instead of padding and emitting a digest.
 constexpr uint32_t kShaResume = 1u;
 constexpr uint32_t kShaPartial = 2u;
+// kShaB64: also write the RFC 4648 Base64 of the message at b64out + b64
+// (fused upload encode; whole messages only, never with Resume/Partial).
+constexpr uint32_t kShaB64 = 4u;
 
 // One byte-stream job for the tiled HBM-bound kernels (Base64 encode/decode,
 // gather, synth).  Jobs are sorted by tile_start; a sentinel job with
@@ -56,10 +60,7 @@ inline uint64_t enc_tiles(uint64_t len) {
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
                          int waves_per_simd, uint32_t* census, hipStream_t s, uint32_t* state = nullptr,
-                         uint32_t rot = 1);
-// Lane-sequence SHA-256: lane l hashes descs[seq[l] .. seq[l+1]) in order.
-hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const uint32_t* seq, uint32_t nlanes,
-                             uint32_t split, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s);
+                         char* b64 = nullptr);
 // Tiles hold per*256 groups (per = 4 or 8, must match the tile count the jobs
 // were built with); nt bit 0 = non-temporal stores, bit 1 = non-temporal loads;
 // pair = 12-bit character-pair LDS table (else the 6-bit alphabet).

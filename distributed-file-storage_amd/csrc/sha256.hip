@@ -161,6 +161,178 @@ __device__ __forceinline__ void init_state(uint32_t (&st)[8]) {
     st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
 }
 
+// ---------------------------------------------------------------------------
+// Fused Base64 (upload plan, fragment lanes flagged kShaB64): the lane that
+// hashes a fragment already holds each 64-byte block in registers as
+// big-endian words, so it also emits the block's Base64 (StorageNode.java:636)
+// instead of a second pass re-reading the fragment from HBM.  Groups of 3
+// bytes straddle blocks with period 3: block k (phase k mod 3, uniform in the
+// wave) encodes 21/21/22 groups = 84/84/88 chars and carries 1/2/0 bytes.
+// Chars come from the 4,096-entry character-pair table in LDS (two reads per
+// group).  The last < 66 bytes (carry + message tail) and the '=' padding are
+// encoded after the block loop by enc_tail.
+
+// x + x on the full-rate adder (hipcc would emit v_lshlrev_b32, half rate).
+__device__ __forceinline__ uint32_t dbl(uint32_t x) {
+    uint32_t r;
+    asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint32_t pair_rd(const uint16_t* __restrict__ pair, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(pair) + byte_addr);
+}
+// Chars of the group at byte q of X = {prev, W[0..15]} (68 bytes, big-endian
+// words): byte addresses 2*hi12 and 2*lo12 straight from the word bits.
+template <int Q>
+__device__ __forceinline__ uint32_t enc_grp(const uint16_t* __restrict__ pair, const uint32_t (&W)[16], uint32_t prev) {
+    constexpr int j = Q / 4, o = Q % 4;
+    const uint32_t x = j == 0 ? prev : W[j == 0 ? 0 : j - 1];
+    const uint32_t y = W[j < 16 ? j : 15];  // X[j+1] (only used for o >= 2, where j < 16)
+    uint32_t ah, al;
+    if (o == 0) {
+        ah = (x >> 19) & 0x1ffeu; al = (x >> 7) & 0x1ffeu;
+    } else if (o == 1) {
+        ah = (x >> 11) & 0x1ffeu; al = dbl(x) & 0x1ffeu;
+    } else if (o == 2) {
+        ah = (x >> 3) & 0x1ffeu; al = __builtin_amdgcn_alignbit(x, y, 23) & 0x1ffeu;
+    } else {
+        ah = __builtin_amdgcn_alignbit(x, y, 27) & 0x1ffeu; al = (y >> 15) & 0x1ffeu;
+    }
+    return __builtin_amdgcn_perm(pair_rd(pair, al), pair_rd(pair, ah), 0x05040100u);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Four groups (8 LDS reads); the scheduling barrier bounds the reads in
+// flight, otherwise hipcc issues all 42 of a block at once (+~60 VGPRs).
+template <int F, int G0>
+__device__ __forceinline__ u32x4 enc_quad(const uint16_t* __restrict__ pair, const uint32_t (&W)[16], uint32_t prev) {
+    const u32x4 r{enc_grp<F + 3 * G0>(pair, W, prev), enc_grp<F + 3 * (G0 + 1)>(pair, W, prev),
+                  enc_grp<F + 3 * (G0 + 2)>(pair, W, prev), enc_grp<F + 3 * (G0 + 3)>(pair, W, prev)};
+    __builtin_amdgcn_sched_barrier(0);
+    return r;
+}
+
+// Block of phase PH (first group at X byte F = 4 - carry_in).  Output is
+// written in whole 128-byte lines of the 256-char super-block sb (3 blocks):
+// phase 0's 21 dwords wait in P, phase 1 writes line 0 (P[0..20] + its first
+// 11 dwords) and keeps its last 10 in P, phase 2 writes line 1 (P[0..9] + its
+// 22).  Each line is stored by 8 back-to-back dwordx4 of the lane, so L2
+// never holds a partly written line across blocks (written block by block,
+// the 64 lanes' interleaved partial lines were evicted half-written:
+// WRITE_SIZE 1.8x and extra fills, 116 vs 82 ms).  With 128-byte aligned
+// fragment starts (DFS_LAYOUT_ALIGN128) every store is a full-line piece.
+template <int PH>
+__device__ __forceinline__ void enc_block(const uint16_t* __restrict__ pair, const uint32_t (&W)[16], uint32_t prev,
+                                          char* __restrict__ sb, uint32_t (&P)[21]) {
+    constexpr int F = PH == 0 ? 4 : (PH == 1 ? 3 : 2);
+    u32x4* d4 = reinterpret_cast<u32x4*>(sb);
+    if (PH == 0) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const u32x4 v = q == 0 ? enc_quad<F, 0>(pair, W, prev)
+                          : q == 1 ? enc_quad<F, 4>(pair, W, prev)
+                          : q == 2 ? enc_quad<F, 8>(pair, W, prev)
+                          : q == 3 ? enc_quad<F, 12>(pair, W, prev)
+                                   : enc_quad<F, 16>(pair, W, prev);
+            P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
+        }
+        P[20] = enc_grp<F + 60>(pair, W, prev);
+    } else if (PH == 1) {
+        const u32x4 n0 = enc_quad<F, 0>(pair, W, prev);
+        const u32x4 n1 = enc_quad<F, 4>(pair, W, prev);
+        const u32x4 n2 = enc_quad<F, 8>(pair, W, prev);
+        d4[0] = u32x4{P[0], P[1], P[2], P[3]};
+        d4[1] = u32x4{P[4], P[5], P[6], P[7]};
+        d4[2] = u32x4{P[8], P[9], P[10], P[11]};
+        d4[3] = u32x4{P[12], P[13], P[14], P[15]};
+        d4[4] = u32x4{P[16], P[17], P[18], P[19]};
+        d4[5] = u32x4{P[20], n0.x, n0.y, n0.z};
+        d4[6] = u32x4{n0.w, n1.x, n1.y, n1.z};
+        d4[7] = u32x4{n1.w, n2.x, n2.y, n2.z};
+        const u32x4 n3 = enc_quad<F, 12>(pair, W, prev);
+        const u32x4 n4 = enc_quad<F, 16>(pair, W, prev);
+        P[0] = n2.w;
+        P[1] = n3.x; P[2] = n3.y; P[3] = n3.z; P[4] = n3.w;
+        P[5] = n4.x; P[6] = n4.y; P[7] = n4.z; P[8] = n4.w;
+        P[9] = enc_grp<F + 60>(pair, W, prev);
+    } else {
+        const u32x4 n0 = enc_quad<F, 0>(pair, W, prev);
+        const u32x4 n1 = enc_quad<F, 4>(pair, W, prev);
+        const u32x4 n2 = enc_quad<F, 8>(pair, W, prev);
+        const u32x4 n3 = enc_quad<F, 12>(pair, W, prev);
+        const u32x4 n4 = enc_quad<F, 16>(pair, W, prev);
+        const uint32_t n20 = enc_grp<F + 60>(pair, W, prev), n21 = enc_grp<F + 63>(pair, W, prev);
+        d4[8] = u32x4{P[0], P[1], P[2], P[3]};
+        d4[9] = u32x4{P[4], P[5], P[6], P[7]};
+        d4[10] = u32x4{P[8], P[9], n0.x, n0.y};
+        d4[11] = u32x4{n0.z, n0.w, n1.x, n1.y};
+        d4[12] = u32x4{n1.z, n1.w, n2.x, n2.y};
+        d4[13] = u32x4{n2.z, n2.w, n3.x, n3.y};
+        d4[14] = u32x4{n3.z, n3.w, n4.x, n4.y};
+        d4[15] = u32x4{n4.z, n4.w, n20, n21};
+    }
+}
+
+// After the block loop: write what enc_block still holds (ph = phase of the
+// next block: 1 -> phase 0's 21 dwords at sb, 2 -> phase 1's last 10 at sb+128).
+__device__ __forceinline__ void enc_flush(uint32_t ph, char* __restrict__ sb, const uint32_t (&P)[21]) {
+    u32x4* d4 = reinterpret_cast<u32x4*>(sb);
+    if (ph == 1) {
+        d4[0] = u32x4{P[0], P[1], P[2], P[3]};
+        d4[1] = u32x4{P[4], P[5], P[6], P[7]};
+        d4[2] = u32x4{P[8], P[9], P[10], P[11]};
+        d4[3] = u32x4{P[12], P[13], P[14], P[15]};
+        d4[4] = u32x4{P[16], P[17], P[18], P[19]};
+        reinterpret_cast<uint32_t*>(sb)[20] = P[20];
+    } else if (ph == 2) {
+        d4[8] = u32x4{P[0], P[1], P[2], P[3]};
+        d4[9] = u32x4{P[4], P[5], P[6], P[7]};
+        *reinterpret_cast<u32x2*>(sb + 160) = u32x2{P[8], P[9]};
+    }
+}
+
+// Bytes [start, len) of the fragment at src, start = 64*nfull - nfull%3 (a
+// multiple of 3): full groups, then the RFC 4648 padded final group.
+__device__ __forceinline__ void enc_tail(const uint16_t* __restrict__ pair, const uint8_t* __restrict__ src,
+                                         uint64_t start, uint64_t len, char* __restrict__ out) {
+    for (uint64_t pos = start; pos < len; pos += 3) {
+        const uint64_t n = len - pos < 3 ? len - pos : 3;
+        uint32_t v = static_cast<uint32_t>(src[pos]) << 16;
+        if (n > 1) v |= static_cast<uint32_t>(src[pos + 1]) << 8;
+        if (n > 2) v |= src[pos + 2];
+        uint32_t w = pair_rd(pair, 2u * (v >> 12)) | (pair_rd(pair, 2u * (v & 0xfffu)) << 16);
+        if (n == 1) w = (w & 0x0000ffffu) | 0x3d3d0000u;       // "xx=="
+        else if (n == 2) w = (w & 0x00ffffffu) | 0x3d000000u;  // "xxx="
+        *reinterpret_cast<uint32_t*>(out + 4 * (pos / 3)) = w;
+    }
+}
+
+__constant__ uint32_t kB64Alpha[16] = {
+    0x44434241u, 0x48474645u, 0x4c4b4a49u, 0x504f4e4du, 0x54535251u, 0x58575655u, 0x62615a59u, 0x66656463u,
+    0x6a696867u, 0x6e6d6c6bu, 0x7271706fu, 0x76757473u, 0x7a797877u, 0x33323130u, 0x37363534u, 0x2f2b3938u};
+
+// Max over the 64 lanes (all active).
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d, 64)));
+    return v;
+}
+
+// Read by lanes with no full block while their wave still runs the block loop.
+__device__ uint32_t g_dummy_block[32];
+
+// Park / restore a lane's 8-word state in LDS (word-major: conflict-free).
+__device__ __forceinline__ void park(uint32_t* stash, const uint32_t (&st)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) stash[i * kShaBlock + threadIdx.x] = st[i];
+}
+__device__ __forceinline__ void unpark(const uint32_t* stash, uint32_t (&st)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = stash[i * kShaBlock + threadIdx.x];
+}
+
 __device__ __forceinline__ uint32_t hw_id() {
     uint32_t v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -190,17 +362,28 @@ __device__ __forceinline__ uint32_t simd_key() {
 // per SIMD, leaving the other wave slots to the Base64 kernel beside it.
 // queue[0] = long counter, queue[1] = short counter, queue[64 + key] = SIMD
 // token counters; all zeroed by the launcher before each launch.
+// ENC = the fused-Base64 instantiation (launched when the caller passes a
+// Base64 output; lanes flagged kShaB64 also write their message's Base64).
+template <bool ENC>
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restrict__ base,
                                                           const ShaDesc* __restrict__ descs, uint32_t n,
                                                           uint32_t split, uint32_t n_long, uint32_t cap,
                                                           uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
                                                           uint32_t* __restrict__ queue,
                                                           uint32_t* __restrict__ census,
-                                                          uint32_t* __restrict__ state, uint32_t rot) {
+                                                          uint32_t* __restrict__ state, char* __restrict__ b64) {
     const uint32_t nitems = (n + 63u) >> 6;
     const uint32_t n_short = nitems - n_long;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t key = simd_key();
+    __shared__ uint16_t pair[ENC ? 4096 : 2];           // Base64 character pairs
+    __shared__ uint32_t stash[ENC ? 8 * kShaBlock : 1];  // states parked by finished lanes
+    if (ENC) {
+        const uint8_t* a = reinterpret_cast<const uint8_t*>(kB64Alpha);
+        for (uint32_t k = threadIdx.x; k < 4096u; k += kShaBlock)
+            pair[k] = static_cast<uint16_t>(a[k >> 6] | (static_cast<uint32_t>(a[k & 63u]) << 8));
+        __syncthreads();
+    }
     for (;;) {
         uint32_t item = 0xffffffffu;
         if (lane == 0) {
@@ -226,6 +409,14 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
         uint64_t t_start = 0;
         if (census) t_start = __builtin_amdgcn_s_memrealtime();
         const uint32_t gid = item * 64u + lane;
+        // ENC: uniform trip count (the wave's longest message, in an SGPR).
+        // A divergent loop exit inside the three-phase body made hipcc copy
+        // the loop state on every exit edge (192 VGPRs, 2 waves/SIMD); lanes
+        // past their own length run the body on a clamped block and park
+        // their state in LDS.
+        const uint32_t kmax =
+            ENC ? __builtin_amdgcn_readfirstlane(wave_max(gid < n ? static_cast<uint32_t>(descs[gid].len >> 6) : 0u))
+                : 0u;
         if (gid < n) {
             const Msg m = msg_setup(base, descs[gid]);
             uint32_t st[8];
@@ -237,15 +428,55 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
             } else {
                 init_state(st);
             }
-            // Short items rotate their issue priority (0/1, flipped every
-            // two blocks): the SIMD arbiter breaks priority ties by wave
-            // age, so without this the oldest short wave of a SIMD runs
-            // ~2x faster than the youngest and the SIMD ends the kernel
-            // with one wave left (tools/census.py).  Flipping on progress
-            // is self-balancing: a wave that ran ahead spends less time at
-            // the higher priority.
-            const bool flip = rot && item >= n_long;
-            if (m.nfull) {
+            if (ENC) {
+                const bool enc = (m.flags & kShaB64) != 0u;
+                char* bdst = b64 + descs[gid].b64;
+                if (kmax) {
+                    // C holds block k, N receives block k+1 (clamped) while C
+                    // is compressed; the body is unrolled over the three
+                    // Base64 phases (k mod 3) so the pending-line registers P
+                    // have static indices; C = N is a register copy.
+                    const uint32_t* bp = m.nfull ? m.p : g_dummy_block;
+                    const uint32_t last = m.nfull ? m.nfull - 1u : 0u;
+                    const bool early = m.nfull < kmax;
+                    if (early) park(stash, st);
+                    uint32_t C[16], N[16], xc, xn;
+                    uint32_t prev = 0;  // last word of the previous block
+                    uint32_t P[21];     // Base64 dwords waiting for their line
+                    load_block(bp, m.sh, C, xc);
+                    uint32_t k = 0;
+#define DFS_SHA_STEP(PH)                                                          \
+    {                                                                             \
+        load_block(bp + 16u * min(k + 1u, last), m.sh, N, xn);                    \
+        to_be(C, xc, m.sel);                                                      \
+        if (enc && k < m.nfull) {                                                 \
+            enc_block<PH>(pair, C, prev, bdst, P);                                \
+            prev = C[15];                                                         \
+        }                                                                         \
+        __builtin_amdgcn_sched_barrier(0); /* keep the encode out of the rounds */ \
+        compress(st, C);                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                        \
+        if (early && k + 1u == m.nfull) park(stash, st);                          \
+        if (++k >= kmax) break;                                                   \
+        _Pragma("unroll") for (int i = 0; i < 16; ++i) C[i] = N[i];               \
+        xc = xn;                                                                  \
+    }
+                    for (;;) {
+                        DFS_SHA_STEP(0)
+                        DFS_SHA_STEP(1)
+                        DFS_SHA_STEP(2)
+                        bdst += 256;
+                    }
+#undef DFS_SHA_STEP
+                    if (early) unpark(stash, st);
+                    if (enc && m.nfull)
+                        enc_flush(m.nfull % 3u, b64 + descs[gid].b64 + 256ull * (m.nfull / 3u), P);
+                }
+                if (enc) {
+                    const uint64_t start = 64ull * m.nfull - m.nfull % 3u;
+                    enc_tail(pair, base + descs[gid].off, start, m.len, b64 + descs[gid].b64);
+                }
+            } else if (m.nfull) {
                 uint32_t A[16], B[16], xa, xb;
                 load_block(m.p, m.sh, A, xa);
                 uint32_t k = 0;
@@ -259,10 +490,6 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
                     to_be(B, xb, m.sel);
                     compress(st, B);
                     if (++k >= m.nfull) break;
-                    if (flip) {
-                        if (k & 2u) __builtin_amdgcn_s_setprio(1);
-                        else __builtin_amdgcn_s_setprio(0);
-                    }
                 }
             }
             if (m.flags & kShaPartial) {  // message continues in a later launch
@@ -289,93 +516,11 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
     }
 }
 
-// Lane sequences: lane l hashes messages seq[l] .. seq[l+1]-1 one after the
-// other, one 64-byte block per loop iteration, with a single compress body.
-// The upload plan pairs, in one wave, the fileId lane of file f (lanes
-// 0..31) with a lane that hashes f's N fragments in order (lanes 32..63):
-// at every iteration both lanes read within 64 bytes of each other in the
-// file, so the second read hits the line the first one brought in (the file
-// crosses HBM once for both chains), and every wave runs the same
-// ceil((S+9)/64)-ish iterations.  Messages switch at per-lane tail blocks
-// (rare, exec-masked branches).
-__device__ __forceinline__ void sha256_seq_lane(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
-                                                const uint32_t* __restrict__ seq, uint32_t l, uint32_t split,
-                                                uint8_t* __restrict__ out0, uint8_t* __restrict__ out1);
-
-__global__ __launch_bounds__(kShaBlock) void sha256_seq(const uint8_t* __restrict__ base,
-                                                        const ShaDesc* __restrict__ descs,
-                                                        const uint32_t* __restrict__ seq, uint32_t nlanes,
-                                                        uint32_t split, uint8_t* __restrict__ out0,
-                                                        uint8_t* __restrict__ out1, uint32_t* __restrict__ census) {
-    const uint32_t l = blockIdx.x * kShaBlock + threadIdx.x;
-    const uint64_t t_start = census ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (l < nlanes) sha256_seq_lane(base, descs, seq, l, split, out0, out1);
-    if (census && (threadIdx.x & 63u) == 0u) {
-        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-        uint32_t* c = census + 4ull * (l >> 6);
-        c[0] = hw_id();
-        c[1] = xcc_id();
-        c[2] = static_cast<uint32_t>(t_start);
-        c[3] = static_cast<uint32_t>(t_end);
-    }
-}
-
-__device__ __forceinline__ void sha256_seq_lane(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
-                                                const uint32_t* __restrict__ seq, uint32_t l, uint32_t split,
-                                                uint8_t* __restrict__ out0, uint8_t* __restrict__ out1) {
-    uint32_t mi = seq[l];
-    const uint32_t mend = seq[l + 1];
-    if (mi >= mend) return;
-    Msg m = msg_setup(base, descs[mi]);
-    uint32_t st[8];
-    init_state(st);
-    uint32_t A[16], B[16], xa = 0, xb = 0;
-    if (m.nfull) load_block(m.p, m.sh, A, xa);
-    uint32_t k = 0;
-    // Two register buffers in ping-pong (the loop body is written twice so no
-    // register copy ever waits on the prefetch): CUR holds block k, NXT
-    // receives block k+1 (or block 0 of the lane's next message).
-#define DFS_SHA_SEQ_STEP(CUR, XC, NXT, XN)                                              \
-    {                                                                                   \
-        uint32_t W[16];                                                                 \
-        if (k < m.nfull) {                                                              \
-            load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, NXT, XN);           \
-            _Pragma("unroll") for (int i = 0; i < 16; ++i) W[i] = CUR[i];               \
-            to_be(W, XC, m.sel);                                                        \
-        } else {                                                                        \
-            tail_block(m, k - m.nfull, W);                                              \
-        }                                                                               \
-        compress(st, W);                                                                \
-        if (++k == m.nfull + m.ntb) { /* message done: publish, start the next one */  \
-            store_digest(st, m.out, split, out0, out1);                                 \
-            if (++mi >= mend) break;                                                    \
-            m = msg_setup(base, descs[mi]);                                             \
-            init_state(st);                                                             \
-            k = 0;                                                                      \
-            if (m.nfull) load_block(m.p, m.sh, NXT, XN);                                \
-        }                                                                               \
-    }
-    for (;;) {
-        DFS_SHA_SEQ_STEP(A, xa, B, xb)
-        DFS_SHA_SEQ_STEP(B, xb, A, xa)
-    }
-#undef DFS_SHA_SEQ_STEP
-}
-
 }  // namespace
-
-hipError_t launch_sha256_seq(const uint8_t* base, const ShaDesc* descs, const uint32_t* seq, uint32_t nlanes,
-                             uint32_t split, uint8_t* out0, uint8_t* out1, uint32_t* census, hipStream_t s) {
-    if (nlanes == 0) return hipSuccess;
-    const uint32_t grid = (nlanes + kShaBlock - 1) / kShaBlock;
-    hipLaunchKernelGGL(sha256_seq, dim3(grid), dim3(kShaBlock), 0, s, base, descs, seq, nlanes, split, out0, out1,
-                       census);
-    return hipGetLastError();
-}
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
-                         uint32_t* census, hipStream_t s, uint32_t* state, uint32_t rot) {
+                         uint32_t* census, hipStream_t s, uint32_t* state, char* b64) {
     if (n == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
     if (e != hipSuccess) return e;
@@ -385,8 +530,13 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     uint64_t waves = 1024ull * static_cast<uint64_t>(waves_per_simd < 1 ? 1 : waves_per_simd);
     if (waves > items) waves = items;
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
-    hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
-                       out1, queue, census, state, rot);
+    if (b64) {
+        hipLaunchKernelGGL(sha256_lanes<true>, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
+                           out0, out1, queue, census, state, b64);
+    } else {
+        hipLaunchKernelGGL(sha256_lanes<false>, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long,
+                           cap, out0, out1, queue, census, state, nullptr);
+    }
     return hipGetLastError();
 }
 

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libdfsgpu.so")
+# DFS_LIB_PATH: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("DFS_LIB_PATH") or os.path.join(PKG_DIR, "libdfsgpu.so")
 REPO_ROOT = os.path.dirname(PKG_DIR)
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "dfs_gpu.h")
 
@@ -29,6 +30,7 @@ DFS_DEVICE_PTRS = 0x1
 DFS_NO_FILEID = 0x2
 DFS_NO_B64 = 0x4
 DFS_SERIAL = 0x8
+DFS_B64_ONLY = 0x80
 DFS_LAYOUT_FRAG_MAJOR = 0x10
 DFS_SHA_BEGIN = 0x20
 DFS_SHA_FINAL = 0x40

@@ -50,7 +50,12 @@ extern "C" {
 #define DFS_DEVICE_PTRS 0x1u    /* data pointers are device pointers; async       */
 #define DFS_NO_FILEID 0x2u      /* upload: skip the whole-file SHA-256            */
 #define DFS_NO_B64 0x4u         /* upload: skip the Base64 encode                 */
-#define DFS_SERIAL 0x8u         /* upload: run SHA and Base64 on one stream       */
+#define DFS_SERIAL 0x8u         /* upload: separate SHA and Base64 kernels, one   */
+                                /* stream (default: Base64 fused into the SHA     */
+                                /* fragment lanes, or DFS_UPLOAD_MODE=kernels:    */
+                                /* the two kernels on two streams)                */
+#define DFS_B64_ONLY 0x80u      /* upload plan: only the Base64 encode kernel     */
+                                /* (measurement of the HBM-bound pass alone)      */
 
 typedef struct dfs_ctx dfs_ctx;
 typedef struct dfs_upload_plan dfs_upload_plan;

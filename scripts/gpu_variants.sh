@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/var
 export TMPDIR=/tmp
-stop_on_fatal() { case "$1" in 0|1) return 0 ;; *) echo "fatal exit $1 -> stopping"; exit "$1" ;; esac; }
+stop_on_fatal() { case "$1" in 0) return 0 ;; *) echo "fatal exit $1 -> stopping"; exit "$1" ;; esac; }
 if [ -z "$SKIP_TESTS" ]; then
   echo "== gpu tests"; timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; stop_on_fatal $rc
 fi

@@ -174,6 +174,53 @@ def test_upload_batch_vs_oracle_mixed_sizes(engine):
                 assert g.b64 == b64[int(off[k]):int(off[k + 1])]
 
 
+def _check_upload(res, files, nfrag):
+    fd, frd, b64, off = O.c_upload_batch(files, nfrag, threads=4)
+    for f, r in enumerate(res):
+        assert r.file_id == fd[f].tobytes().hex()
+        for i, g in enumerate(r.fragments):
+            k = f * nfrag + i
+            assert g.hash == frd[f, i].tobytes().hex(), (len(files[f]), i)
+            assert g.b64 == b64[int(off[k]):int(off[k + 1])], (len(files[f]), i)
+
+
+def test_fused_encode_every_block_phase(monkeypatch):
+    """DFS_UPLOAD_MODE=fused (Base64 written by the SHA fragment lanes):
+    fragments of 0..7 full 64-byte blocks (every block phase k mod 3 and
+    carry) plus every tail class, at the byte alignments the batch packing
+    produces; then mixed lengths inside one wave (lanes leaving the block
+    loop at different blocks park their state)."""
+    monkeypatch.setenv("DFS_UPLOAD_MODE", "fused")
+    eng = dfs_amd.FragmentEngine(0)
+    try:
+        sizes = [64 * k + r for k in range(8) for r in (0, 1, 2, 3, 5, 55, 56, 63)]
+        for nfrag in (1, 3, 5):
+            files = [O.c_synth(3000 + i, 0, s * nfrag + (i % nfrag)) for i, s in enumerate(sizes)]
+            _check_upload(eng.upload(files, nfrag), files, nfrag)
+        rng = random.Random(17)
+        files = [O.c_synth(3500 + i, 0, rng.randrange(0, 6000)) for i in range(200)]
+        _check_upload(eng.upload(files, 5), files, 5)
+        sizes = [rng.choice([0, 7, 64, 200, 4099, 65536, 300001]) for _ in range(40)]
+        files = [O.c_synth(3800 + i, 0, s) for i, s in enumerate(sizes)]
+        _check_upload(eng.upload(files, 4), files, 4)
+    finally:
+        eng.close()
+
+
+def test_upload_two_kernel_mode(monkeypatch):
+    """DFS_UPLOAD_MODE=kernels (the library default): SHA-256 and the Base64
+    encode kernel on two streams."""
+    monkeypatch.setenv("DFS_UPLOAD_MODE", "kernels")
+    eng = dfs_amd.FragmentEngine(0)
+    try:
+        rng = random.Random(5)
+        sizes = [rng.choice([0, 7, 64, 200, 4099, 65536, 300001]) for _ in range(40)]
+        files = [O.c_synth(4000 + i, 0, s) for i, s in enumerate(sizes)]
+        _check_upload(eng.upload(files, 5), files, 5)
+    finally:
+        eng.close()
+
+
 def test_reassemble_verify(engine, example_bytes):
     files = [example_bytes["id.jpg"], example_bytes["teste.txt"], O.c_synth(9, 0, 100003)]
     ups = engine.upload(files, 5)
@@ -338,7 +385,9 @@ def test_profiling_timings(engine):
         engine.upload([O.c_synth(3, 0, 1 << 20)] * 8, 5)
         t = engine.timings()
         assert t["sha"] is not None and t["sha"] > 0
-        assert t["b64enc"] is not None and t["b64enc"] > 0
+        assert t["total"] is not None and t["total"] >= t["sha"] * 0.99
+        if t["b64enc"] is not None:  # two-kernel upload (the fused mode has no separate encode)
+            assert t["b64enc"] > 0
     finally:
         engine.set_profiling(False)
 
