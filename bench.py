@@ -65,6 +65,8 @@ def parse():
                     help="kernels: SHA and Base64 kernels on two streams (default); fused: Base64 "
                          "written by the SHA fragment lanes; serial: the two kernels on one stream")
     ap.add_argument("--serial", action="store_true", help="alias of --mode serial")
+    ap.add_argument("--align128", action=argparse.BooleanOptionalAction, default=False,
+                    help="DFS_LAYOUT_ALIGN128: every fragment's Base64 starts on a 128-byte boundary")
     ap.add_argument("--b64-steps", type=int, default=3, help="steps of the standalone Base64 leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
@@ -194,8 +196,7 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
     import numpy as np
     import torch
     from dfs_amd.engine import download_device
-    offs = plan.b64_offsets()
-    msp = np.stack([offs[:-1], offs[1:] - offs[:-1]], axis=1).astype(np.uint64)
+    msp = plan.b64_spans([S] * F)
     file_len = np.full(F, S, dtype=np.uint64)
     file_off = np.arange(F, dtype=np.uint64) * np.uint64(S)
     out = torch.empty(F * S, dtype=torch.uint8, device=dev)
@@ -222,7 +223,7 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
     del out
     dev_ms = float(np.mean(tot))
     dec_ms = float(np.mean(dec))
-    dec_bytes = int(offs[-1]) + F * S  # Base64 read + bytes written
+    dec_bytes = int(msp[:, 1].sum()) + F * S  # Base64 read + bytes written
     log(f"download: {F} files, device {dev_ms:.1f} ms (decode {dec_ms:.1f}, sha {np.mean(sha):.1f}), ok={ok}")
     return {"files_per_gpu": F, "device_ms": round(dev_ms, 3), "wall_ms": round(float(np.mean(wall)) * 1e3, 3),
             "gbps": round(F * S / (dev_ms / 1e3) / 1e9, 2),
@@ -261,7 +262,7 @@ def main():
     first_file = rank * F  # this rank's shard of the global file set
     files = torch.empty(F * S + 64, dtype=torch.uint8, device=dev)
     dfs_amd.synth_fill(eng, files.data_ptr(), spans, first_file, SEED)
-    plan = dfs_amd.UploadPlan(eng, spans, N)
+    plan = dfs_amd.UploadPlan(eng, spans, N, align128=args.align128)
     fd = torch.empty(F * 32, dtype=torch.uint8, device=dev)
     frd = torch.empty(F * N * 32, dtype=torch.uint8, device=dev)
     b64 = torch.empty(plan.b64_total, dtype=torch.uint8, device=dev)
@@ -313,14 +314,14 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # checker only
         idx = sorted(set([0, F - 1] + list(np.random.default_rng(1).integers(0, F, args.verify))))
-        offs = plan.b64_offsets()
+        bsp = plan.b64_spans([S] * F)
         fdh = fd.view(F, 32).cpu().numpy()
         frdh = frd.view(F, N, 32).cpu().numpy()
         for f in idx:
             data = O.c_synth(first_file + f, 0, S)
             efd, efrd, eb64, eoff = O.c_upload_batch([data], N)
             k0 = f * N
-            got_b64 = b64[int(offs[k0]):int(offs[k0 + N])].cpu().numpy().tobytes()
+            got_b64 = b"".join(b64[int(o):int(o + n)].cpu().numpy().tobytes() for o, n in bsp[k0:k0 + N])
             if not ((fdh[f] == efd[0]).all() and (frdh[f] == efrd[0]).all() and got_b64 == eb64):
                 ok = False
         log(f"oracle spot-check of {len(idx)} files: {'OK' if ok else 'MISMATCH'}")
@@ -334,7 +335,7 @@ def main():
     b64_avg = float(np.mean(b64_ms)) / 1e3
     achieved_tops = blocks * OPS_PER_BLOCK_CANON / sha_avg / 1e12
     issued_tops = blocks * OPS_PER_BLOCK_ISSUED / sha_avg / 1e12
-    b64_bytes = F * S + plan.b64_total
+    b64_bytes = F * S + 4 * F * sum((x + 2) // 3 for x in lens)  # read + Base64 written
     b64_gbs = b64_bytes / b64_avg / 1e9
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -363,7 +364,8 @@ def main():
                    "files_per_gpu": F, "file_bytes": S, "nfrag": N,
                    "mode": {"fused": "Base64 fused into the SHA-256 fragment lanes (one kernel)",
                             "kernels": "SHA-256 || Base64 kernels on two streams",
-                            "serial": "SHA-256 then Base64 kernel, one stream"}[args.mode]},
+                            "serial": "SHA-256 then Base64 kernel, one stream"}[args.mode],
+                   "b64_layout": "128-byte aligned fragment starts" if args.align128 else "packed"},
         "roofline": {"bound": "valu", "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 3),
                      "unit": "Tops/s (int32)", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
                      "traffic": traffic, "kernel": "sha256_lanes" + (" (+ fused Base64)" if args.mode == "fused" else ""),

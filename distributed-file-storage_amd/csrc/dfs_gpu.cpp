@@ -559,8 +559,9 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
 int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint32_t flags,
                            dfs_upload_plan** out, uint64_t* b64_total) {
     if (!c || !out || !nfrag || (nfiles && !files)) return DFS_E_ARG;
-    if (flags & ~DFS_LAYOUT_FRAG_MAJOR) return DFS_E_ARG;
+    if (flags & ~(DFS_LAYOUT_FRAG_MAJOR | DFS_LAYOUT_ALIGN128)) return DFS_E_ARG;
     const bool frag_major = flags & DFS_LAYOUT_FRAG_MAJOR;
+    const uint64_t align = (flags & DFS_LAYOUT_ALIGN128) ? 128 : 1;
     *out = nullptr;
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = enter(c)) return rc;
@@ -602,6 +603,7 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     auto place = [&](uint32_t f, uint32_t i) {
         const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
         const ShaDesc& d = frag[k];
+        total = (total + align - 1) / align * align;
         p->b64_off[k] = total;
         if (d.len) {
             StreamJob j{};

@@ -32,6 +32,7 @@ DFS_NO_B64 = 0x4
 DFS_SERIAL = 0x8
 DFS_B64_ONLY = 0x80
 DFS_LAYOUT_FRAG_MAJOR = 0x10
+DFS_LAYOUT_ALIGN128 = 0x100
 DFS_SHA_BEGIN = 0x20
 DFS_SHA_FINAL = 0x40
 

@@ -356,23 +356,35 @@ def download_device(engine: "FragmentEngine", d_b64: int, spans: np.ndarray, nfi
 class UploadPlan:
     """dfs_upload_plan over device-resident (torch) buffers — the bench path."""
 
-    def __init__(self, engine: FragmentEngine, spans: np.ndarray, nfrag: int, frag_major: bool = False):
+    def __init__(self, engine: FragmentEngine, spans: np.ndarray, nfrag: int, frag_major: bool = False,
+                 align128: bool = False):
         self.engine = engine
         spans = np.ascontiguousarray(spans, dtype=np.uint64)
         self.nfiles = len(spans)
         self.nfrag = nfrag
         self.frag_major = frag_major
+        self.align128 = align128
         self._plan = ctypes.c_void_p()
         total = ctypes.c_uint64(0)
-        flags = L.DFS_LAYOUT_FRAG_MAJOR if frag_major else 0
+        flags = (L.DFS_LAYOUT_FRAG_MAJOR if frag_major else 0) | (L.DFS_LAYOUT_ALIGN128 if align128 else 0)
         check(lib().dfs_upload_plan_create(engine.ctx, _ptr(spans), self.nfiles, nfrag, flags,
                                            ctypes.byref(self._plan), ctypes.byref(total)), "dfs_upload_plan_create")
         self.b64_total = total.value
 
     def b64_offsets(self) -> np.ndarray:
+        """nfiles*nfrag+1 offsets (fragment start; last = total)."""
         off = np.zeros(self.nfiles * self.nfrag + 1, dtype=np.uint64)
         check(lib().dfs_upload_plan_b64_offsets(self._plan, _ptr(off)), "dfs_upload_plan_b64_offsets")
         return off
+
+    def b64_spans(self, file_lens) -> np.ndarray:
+        """(start, length) of every fragment's Base64 in [file][fragment]
+        order; lengths come from the split, so they are exact with the
+        align128 gaps too."""
+        off = self.b64_offsets()
+        lens = np.array([4 * ((ln + 2) // 3) for fl in file_lens for _, ln in split_plan(int(fl), self.nfrag)],
+                        dtype=np.uint64)
+        return np.stack([off[:-1], lens], axis=1).astype(np.uint64)
 
     def run(self, d_files: int, d_file_digest: int, d_frag_digest: int, d_b64: int, flags: int = 0) -> None:
         check(lib().dfs_upload_plan_run(self.engine.ctx, self._plan, ctypes.c_void_p(d_files),

@@ -190,6 +190,10 @@ int dfs_download_batch(dfs_ctx* ctx, const char* b64, const dfs_span* b64_msgs, 
  * contiguously ([fragment][file] order) so the bytes bound for one node are
  * one span (multi-GPU placement exchange); default is [file][fragment]. */
 #define DFS_LAYOUT_FRAG_MAJOR 0x10u
+/* DFS_LAYOUT_ALIGN128 starts every fragment's Base64 on a 128-byte boundary
+ * (gaps between fragments are left unwritten): the fused upload then stores
+ * whole 128-byte lines.  Fragment ends are start + dfs_b64_encoded_len. */
+#define DFS_LAYOUT_ALIGN128 0x100u
 int dfs_upload_plan_create(dfs_ctx* ctx, const dfs_span* file_spans, uint32_t nfiles, uint32_t nfrag,
                            uint32_t flags, dfs_upload_plan** plan, uint64_t* b64_total);
 /* Copy the plan's Base64 offsets to host memory: nfiles*nfrag+1 entries,

@@ -294,6 +294,56 @@ def test_device_plan_and_synth_vs_oracle(engine):
         plan.close()
 
 
+@pytest.mark.parametrize("mode", ["kernels", "fused"])
+def test_align128_plan(monkeypatch, mode):
+    """DFS_LAYOUT_ALIGN128: fragment Base64 starts on 128-byte boundaries,
+    bytes identical to the oracle, gap bytes untouched, and the download path
+    reads the fragments back through b64_spans."""
+    import torch
+    from dfs_amd.engine import download_device
+    monkeypatch.setenv("DFS_UPLOAD_MODE", mode)
+    eng = dfs_amd.FragmentEngine(0)
+    nfiles, nfrag = 60, 5
+    rng = random.Random(128)
+    lens = [rng.choice([0, 1, 100, 4096, 70001, 123457]) for _ in range(nfiles)]
+    offs_f = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    spans = np.stack([offs_f[:-1], np.array(lens, dtype=np.uint64)], axis=1)
+    files = torch.empty(int(offs_f[-1]) + 64, dtype=torch.uint8, device="cuda")
+    dfs_amd.synth_fill(eng, files.data_ptr(), spans, 900, O.SYNTH_SEED)
+    plan = dfs_amd.UploadPlan(eng, spans, nfrag, align128=True)
+    try:
+        fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
+        frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
+        b64 = torch.full((plan.b64_total,), 0xAA, dtype=torch.uint8, device="cuda")
+        plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
+        torch.cuda.synchronize()
+        bsp = plan.b64_spans(lens)
+        assert (bsp[:, 0] % 128 == 0).all()
+        host = files.cpu().numpy()
+        blob = b64.cpu().numpy().tobytes()
+        files_b = [host[int(o):int(o) + ln].tobytes() for o, ln in zip(offs_f[:-1], lens)]
+        efd, efrd, _, _ = O.c_upload_batch(files_b, nfrag)
+        assert (fd.cpu().numpy().reshape(nfiles, 32) == efd).all()
+        assert (frd.cpu().numpy().reshape(nfiles, nfrag, 32) == efrd).all()
+        covered = np.zeros(len(blob), dtype=bool)
+        for f, d in enumerate(files_b):
+            for i, (o, ln) in enumerate(O.c_split(len(d), nfrag)):
+                so, sl = (int(x) for x in bsp[f * nfrag + i])
+                assert blob[so:so + sl] == O.c_b64_encode(d[o:o + ln])
+                covered[so:so + sl] = True
+        gaps = np.frombuffer(blob, dtype=np.uint8)[~covered]
+        assert (gaps == 0xAA).all()
+        out = torch.zeros(int(offs_f[-1]) + 1, dtype=torch.uint8, device="cuda")
+        st = download_device(eng, b64.data_ptr(), bsp, nfiles, nfrag, np.array(lens, dtype=np.uint64),
+                             frd.data_ptr(), fd.data_ptr(), out.data_ptr(), offs_f[:-1].copy())
+        torch.cuda.synchronize()
+        assert (st == 0).all()
+        assert torch.equal(out[:int(offs_f[-1])], files[:int(offs_f[-1])])
+    finally:
+        plan.close()
+        eng.close()
+
+
 def test_frag_major_plan_and_device_download(engine):
     """The single-GPU half of bench.py's placement leg: a fragment-major
     upload plan, then dfs_download_batch on device pointers over the
