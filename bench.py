@@ -65,7 +65,7 @@ def parse():
                     help="kernels: SHA and Base64 kernels on two streams (default); fused: Base64 "
                          "written by the SHA fragment lanes; serial: the two kernels on one stream")
     ap.add_argument("--serial", action="store_true", help="alias of --mode serial")
-    ap.add_argument("--align128", action=argparse.BooleanOptionalAction, default=False,
+    ap.add_argument("--align128", action=argparse.BooleanOptionalAction, default=True,
                     help="DFS_LAYOUT_ALIGN128: every fragment's Base64 starts on a 128-byte boundary")
     ap.add_argument("--b64-steps", type=int, default=3, help="steps of the standalone Base64 leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -62,10 +62,11 @@ struct dfs_ctx {
     hipStream_t user = nullptr;  // borrowed (dfs_set_stream)
     bool profiling = false;
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
+    int sha_wps_beside = 3;      // ... when the Base64 kernel runs beside it (4 x 116 VGPRs leave no room)
     int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels (DFS_UPLOAD_MODE)
     int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
-    int b64_nt = 1;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
+    int b64_nt = 3;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
     bool b64_pair = true;        // 12-bit pair table (DFS_B64_LUT=12) vs 6-bit alphabet (=6)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
@@ -224,7 +225,7 @@ int dfs_open(dfs_ctx** out, int device) {
     dfs_ctx* c = new (std::nothrow) dfs_ctx;
     if (!c) return DFS_E_NOMEM;
     c->device = device;
-    if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = std::max(1, std::min(8, std::atoi(w)));
+    if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = c->sha_wps_beside = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_UPLOAD_MODE")) c->upload_mode = std::strcmp(w, "fused") == 0 ? 0 : 1;
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
@@ -710,6 +711,7 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
         HIPC(hipMemsetAsync(census, 0, 16ull * n_items, s));
     }
     const bool two = do_b64 && !fused;  // separate Base64 encode kernel
+    const int wps = two && !serial ? c->sha_wps_beside : c->sha_wps;
     tm.begin(DFS_T_TOTAL, s);
     if (two && !serial) {  // fork: Base64 on the aux stream beside SHA
         HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER], s));
@@ -720,10 +722,10 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     tm.begin(DFS_T_SHA, s);
     if (do_fileid) {
         HIPC(dfs::launch_sha256(d_files, p->d_all, p->n_all, p->nfiles, p->prio_all, d_fd, d_frd, p->d_queue,
-                                c->sha_wps, census, s, nullptr, fb64));
+                                wps, census, s, nullptr, fb64));
     } else {
         HIPC(dfs::launch_sha256(d_files, p->d_frag, p->n_frag_only, p->nfiles, p->prio_frag, d_fd, d_frd,
-                                p->d_queue, c->sha_wps, census, s, nullptr, fb64));
+                                p->d_queue, wps, census, s, nullptr, fb64));
     }
     tm.end(DFS_T_SHA, s);
     if (two) {

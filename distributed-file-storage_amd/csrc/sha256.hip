@@ -20,6 +20,8 @@
 //    current one is compressed (two register buffers, loop unrolled x2).
 #include "dfs_internal.h"
 
+#include <cstdlib>
+
 namespace dfs {
 namespace {
 
@@ -364,14 +366,12 @@ __device__ __forceinline__ uint32_t simd_key() {
 // token counters; all zeroed by the launcher before each launch.
 // ENC = the fused-Base64 instantiation (launched when the caller passes a
 // Base64 output; lanes flagged kShaB64 also write their message's Base64).
-template <bool ENC>
-__global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restrict__ base,
-                                                          const ShaDesc* __restrict__ descs, uint32_t n,
-                                                          uint32_t split, uint32_t n_long, uint32_t cap,
-                                                          uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
-                                                          uint32_t* __restrict__ queue,
-                                                          uint32_t* __restrict__ census,
-                                                          uint32_t* __restrict__ state, char* __restrict__ b64) {
+template <bool ENC, int LOOP>
+__device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
+                                            uint32_t n, uint32_t split, uint32_t n_long, uint32_t cap,
+                                            uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
+                                            uint32_t* __restrict__ queue, uint32_t* __restrict__ census,
+                                            uint32_t* __restrict__ state, char* __restrict__ b64) {
     const uint32_t nitems = (n + 63u) >> 6;
     const uint32_t n_short = nitems - n_long;
     const uint32_t lane = threadIdx.x & 63u;
@@ -476,7 +476,38 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
                     const uint64_t start = 64ull * m.nfull - m.nfull % 3u;
                     enc_tail(pair, base + descs[gid].off, start, m.len, b64 + descs[gid].b64);
                 }
-            } else if (m.nfull) {
+            } else if (m.nfull && LOOP == 1) {
+                // Blocks are fetched in pairs (2j, 2j+1) requested back to
+                // back — one 128-byte line for line-aligned messages, so L2
+                // never has to keep a half-read line across a compression —
+                // and the next pair is in flight while the current pair is
+                // compressed (two pairs of register buffers, loop unrolled
+                // x4).  Beside the Base64 stream this cut the SHA kernel's
+                // re-reads and its stalls on loaded HBM.
+                uint32_t A[16], B[16], C[16], D[16], xa, xb, xc, xd;
+                const uint32_t last = m.nfull - 1u;
+                load_block(m.p, m.sh, A, xa);
+                load_block(m.p + 16u * min(1u, last), m.sh, B, xb);
+                uint32_t k = 0;
+                for (;;) {
+                    load_block(m.p + 16u * min(k + 2u, last), m.sh, C, xc);
+                    load_block(m.p + 16u * min(k + 3u, last), m.sh, D, xd);
+                    to_be(A, xa, m.sel);
+                    compress(st, A);
+                    if (++k >= m.nfull) break;
+                    to_be(B, xb, m.sel);
+                    compress(st, B);
+                    if (++k >= m.nfull) break;
+                    load_block(m.p + 16u * min(k + 2u, last), m.sh, A, xa);
+                    load_block(m.p + 16u * min(k + 3u, last), m.sh, B, xb);
+                    to_be(C, xc, m.sel);
+                    compress(st, C);
+                    if (++k >= m.nfull) break;
+                    to_be(D, xd, m.sel);
+                    compress(st, D);
+                    if (++k >= m.nfull) break;
+                }
+            } else if (m.nfull && LOOP == 0) {
                 uint32_t A[16], B[16], xa, xb;
                 load_block(m.p, m.sh, A, xa);
                 uint32_t k = 0;
@@ -490,6 +521,20 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
                     to_be(B, xb, m.sel);
                     compress(st, B);
                     if (++k >= m.nfull) break;
+                }
+            } else if (m.nfull) {
+                // One compression per iteration (half the code of LOOP 0):
+                // C = N is a register copy.
+                uint32_t C[16], N[16], xc, xn;
+                load_block(m.p, m.sh, C, xc);
+                for (uint32_t k = 0;;) {
+                    load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, N, xn);
+                    to_be(C, xc, m.sel);
+                    compress(st, C);
+                    if (++k >= m.nfull) break;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) C[i] = N[i];
+                    xc = xn;
                 }
             }
             if (m.flags & kShaPartial) {  // message continues in a later launch
@@ -516,6 +561,26 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes(const uint8_t* __restr
     }
 }
 
+#define DFS_SHA_ARGS                                                                                     \
+    const uint8_t *__restrict__ base, const ShaDesc *__restrict__ descs, uint32_t n, uint32_t split,       \
+        uint32_t n_long, uint32_t cap, uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,             \
+        uint32_t *__restrict__ queue, uint32_t *__restrict__ census, uint32_t *__restrict__ state,         \
+        char *__restrict__ b64
+// Plain (hash only).  LOOP = block-loop shape: 1 (default) pair-fetch with
+// four buffers, 0 two register buffers (unrolled x2), 2 one compression per
+// iteration (DFS_SHA_LOOP selects; experiment hook).  Measured, config 2
+// alone: 76.6 / 78.8 / 79.4 ms; beside Base64 (3 / 4 / 4 waves): 91.3 /
+// 93.1 / 93.9 ms.
+template <int LOOP>
+__global__ __launch_bounds__(kShaBlock) void sha256_lanes(DFS_SHA_ARGS) {
+    sha256_body<false, LOOP>(base, descs, n, split, n_long, cap, out0, out1, queue, census, state, b64);
+}
+// Fused: fragment lanes flagged kShaB64 also write their Base64.
+__global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
+    sha256_body<true, 0>(base, descs, n, split, n_long, cap, out0, out1, queue, census, state, b64);
+}
+#undef DFS_SHA_ARGS
+
 }  // namespace
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
@@ -531,10 +596,15 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     if (waves > items) waves = items;
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     if (b64) {
-        hipLaunchKernelGGL(sha256_lanes<true>, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
+        hipLaunchKernelGGL(sha256_lanes_b64, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
                            out0, out1, queue, census, state, b64);
     } else {
-        hipLaunchKernelGGL(sha256_lanes<false>, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long,
+        static const int loop = [] {
+            const char* v = std::getenv("DFS_SHA_LOOP");
+            return v ? std::atoi(v) : 1;
+        }();
+        auto k = loop == 1 ? sha256_lanes<1> : loop == 2 ? sha256_lanes<2> : sha256_lanes<0>;
+        hipLaunchKernelGGL(k, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long,
                            cap, out0, out1, queue, census, state, nullptr);
     }
     return hipGetLastError();
