@@ -440,6 +440,39 @@ int dfs_receive_fragments_batch(dfs_ctx* c, const char* in, const dfs_span* msgs
 }
 
 // ---------------------------------------------------------------------------
+int dfs_sha256_update_parts(dfs_ctx* c, const uint8_t* base, const dfs_part* parts, uint32_t n, uint32_t* state,
+                            uint8_t* digests, uint32_t flags) {
+    if (!c || !(flags & DFS_DEVICE_PTRS) || (n && (!parts || !state || !digests))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!n) return DFS_OK;
+    hipStream_t s = c->stream();
+    std::vector<ShaDesc> d(n);
+    uint64_t end = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const dfs_part& q = parts[i];
+        const bool fin = q.flags & DFS_SHA_FINAL;
+        if (q.len >= kMaxMsg || (!fin && (q.len & 63u)) || (fin && q.total < q.len)) return DFS_E_ARG;
+        d[i] = ShaDesc{q.off, q.len, fin ? q.total : q.len, q.slot,
+                       ((q.flags & DFS_SHA_BEGIN) ? 0u : dfs::kShaResume) | (fin ? 0u : dfs::kShaPartial), 0};
+        end = std::max(end, q.off + q.len);
+    }
+    if (end && !base) return DFS_E_ARG;
+    const uint32_t prio = sort_lanes(d);
+    if (int rc = put(c, B_DESC, d.data(), d.size() * sizeof(ShaDesc), s)) return rc;
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_SHA, s);
+    // digests indexed by slot: split = UINT32_MAX keeps every slot in out0
+    HIPC(dfs::launch_sha256(base, c->buf[B_DESC].as<ShaDesc>(), n, UINT32_MAX, prio, digests, digests,
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, state));
+    tm.end(DFS_T_SHA, s);
+    tm.end(DFS_T_TOTAL, s);
+    return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
 int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint32_t n, char* out,
                          uint64_t out_cap, uint64_t* out_off, uint32_t flags) {
     if (!c || !out_off || (n && !msgs)) return DFS_E_ARG;
@@ -1016,7 +1049,12 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
 
 // ---------------------------------------------------------------------------
 int dfs_synth_fill(dfs_ctx* c, uint8_t* d_dst, const dfs_span* files, uint32_t nfiles, uint64_t first, uint64_t seed) {
-    if (!c || (nfiles && (!files || !d_dst))) return DFS_E_ARG;
+    return dfs_synth_fill_at(c, d_dst, files, nfiles, first, seed, 0);
+}
+
+int dfs_synth_fill_at(dfs_ctx* c, uint8_t* d_dst, const dfs_span* files, uint32_t nfiles, uint64_t first,
+                      uint64_t seed, uint64_t file_off) {
+    if (!c || (nfiles && (!files || !d_dst)) || (file_off & 7u)) return DFS_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = enter(c)) return rc;
     if (!nfiles) return DFS_OK;
@@ -1035,7 +1073,7 @@ int dfs_synth_fill(dfs_ctx* c, uint8_t* d_dst, const dfs_span* files, uint32_t n
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
     const uint64_t ntiles = finish_jobs(jobs, items, dfs::kStreamBlock);
     if (int rc = put(c, B_JOBS2, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
-    HIPC(dfs::launch_synth(d_dst, c->buf[B_JOBS2].as<StreamJob>(), njobs, ntiles, seed, s));
+    HIPC(dfs::launch_synth(d_dst, c->buf[B_JOBS2].as<StreamJob>(), njobs, ntiles, seed, s, file_off));
     HIPC(hipStreamSynchronize(s));  // the job table lives in reusable scratch
     return DFS_OK;
 }

@@ -76,8 +76,8 @@ hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njo
 // Gather: job.src_off is an absolute device address of the fragment.
 hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
                          hipStream_t s);
-hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                        uint64_t seed, hipStream_t s);
+hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
+                        hipStream_t s, uint64_t file_off);
 // Compare n digests a[i] vs b[i] (32 B each); status[i*stride] = code if different.
 hipError_t launch_digest_compare(const uint8_t* a, const uint8_t* b, uint32_t n, int32_t code,
                                  int32_t* status, uint32_t status_div, hipStream_t s);

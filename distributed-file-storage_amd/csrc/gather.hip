@@ -62,7 +62,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // Item c covers file bytes [64c, 64c+64).
 __global__ __launch_bounds__(kStreamBlock) void synth_kernel(uint8_t* __restrict__ dst_base,
                                                              const StreamJob* __restrict__ jobs, uint32_t njobs,
-                                                             uint64_t ntiles, uint64_t seed) {
+                                                             uint64_t ntiles, uint64_t seed, uint64_t file_off) {
     uint64_t t0, t1;
     tile_range(ntiles, t0, t1);
     if (t0 >= t1) return;
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(kStreamBlock) void synth_kernel(uint8_t* __restrict
         for (int k = 0; k < 8; ++k) {
             const uint64_t o = b0 + 8 * k;
             if (o >= len) break;
-            const uint64_t v = splitmix64(seed ^ ((f << 40) | (o >> 3)));
+            const uint64_t v = splitmix64(seed ^ ((f << 40) | ((file_off + o) >> 3)));  // file_off % 8 == 0
             if (aligned && o + 8 <= len) {
                 *reinterpret_cast<uint64_t*>(dst + o) = v;
             } else {
@@ -110,10 +110,10 @@ hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
 }
 
 hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
-                        hipStream_t s) {
+                        hipStream_t s, uint64_t file_off) {
     if (ntiles == 0) return hipSuccess;
     hipLaunchKernelGGL(synth_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, dst, jobs, njobs, ntiles,
-                       seed);
+                       seed, file_off);
     return hipGetLastError();
 }
 

@@ -76,6 +76,8 @@ SIGNATURES = {
     "dfs_upload_plan_run": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_upload_plan_destroy": (_int, [_vp]),
     "dfs_synth_fill": (_int, [_vp, _vp, _vp, _u32, _u64, _u64]),
+    "dfs_sha256_update_parts": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _u32]),
+    "dfs_synth_fill_at": (_int, [_vp, _vp, _vp, _u32, _u64, _u64, _u64]),
 }
 
 _LIB = None

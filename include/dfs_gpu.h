@@ -119,6 +119,26 @@ int dfs_sha256_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* msgs, ui
 int dfs_sha256_update_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* parts, uint32_t n,
                             uint32_t* state, const uint64_t* total_len, uint8_t* digests, uint32_t flags);
 
+/* Streaming SHA-256 with per-part state slots and flags: one call advances
+ * any subset of a larger set of messages, each at its own stage (the chunked
+ * upload of files larger than HBM, BASELINE config 4, where fragment i of a
+ * file begins and ends in different chunks than the file's fileId message).
+ *   parts[i].off/len  bytes of this part (base + off); len % 64 == 0 unless
+ *                     DFS_SHA_FINAL is set in parts[i].flags
+ *   parts[i].total    whole-message length (used with DFS_SHA_FINAL)
+ *   parts[i].slot     message index: state + 8*slot, digests + 32*slot
+ *   parts[i].flags    DFS_SHA_BEGIN (start from H0, state not read) and/or
+ *                     DFS_SHA_FINAL (pad, write the digest, state not written)
+ * A slot may appear at most once per call.  `base`, `state`, `digests` are
+ * device pointers (DFS_DEVICE_PTRS is required); the call is asynchronous on
+ * the ctx stream.  Same kernel as dfs_sha256_batch (sha256_lanes). */
+typedef struct dfs_part {
+    uint64_t off, len, total;
+    uint32_t slot, flags;
+} dfs_part;
+int dfs_sha256_update_parts(dfs_ctx* ctx, const uint8_t* base, const dfs_part* parts, uint32_t n,
+                            uint32_t* state, uint8_t* digests, uint32_t flags);
+
 /* Base64.getEncoder().encodeToString at SN:636 for `n` messages.  Output i is
  * written at out + out_off[i]; out_off (n+1 entries) is computed by the
  * library as the prefix sum of dfs_b64_encoded_len and returned. */
@@ -211,6 +231,11 @@ int dfs_upload_plan_destroy(dfs_upload_plan* plan);
  * d_dst + file_spans[f].off (device pointer). */
 int dfs_synth_fill(dfs_ctx* ctx, uint8_t* d_dst, const dfs_span* file_spans, uint32_t nfiles,
                    uint64_t first_file_index, uint64_t seed);
+/* As dfs_synth_fill, but the bytes written at d_dst + file_spans[f].off are
+ * those of file offsets [file_off, file_off + len) (file_off % 8 == 0): one
+ * chunk of files larger than HBM (BASELINE config 4). */
+int dfs_synth_fill_at(dfs_ctx* ctx, uint8_t* d_dst, const dfs_span* file_spans, uint32_t nfiles,
+                      uint64_t first_file_index, uint64_t seed, uint64_t file_off);
 
 #ifdef __cplusplus
 }
