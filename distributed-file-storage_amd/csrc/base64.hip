@@ -192,37 +192,13 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
 }
 
 // ---------------------------------------------------------------------------
-// Decode.
+// Decode (geometry: dec_geom in dfs_internal.h).
 // Message of L chars: q = L/4 full units, r = L%4.
 //   r == 1           -> IllegalArgumentException (dangling char / bad ending)
 //   r == 2, 3        -> q body units + a final unit of r alphabet chars
 //   r == 0, q >= 1   -> q-1 body units + a final unit "xxxx" | "xxx=" | "xx=="
 // Body units must be 4 alphabet chars.  Output byte i goes to dst + i.
-// With h = bytes up to the first 4-aligned output address, item c < nc writes
-// output bytes [h+12c, h+12c+12) as three aligned dwords; item nc (the "tail"
-// item) writes the head and tail bytes, decodes the final unit, validates
-// the body units no main item owns and sets status / out_len.
 // ---------------------------------------------------------------------------
-struct DecGeom {
-    uint64_t body_units;
-    uint64_t nb;   // body bytes
-    uint32_t h;    // head bytes
-    uint64_t nc;   // main items
-    uint32_t u_first;  // first unit owned by main items (h == 3)
-};
-
-__device__ __forceinline__ DecGeom dec_geom(uint64_t L, uintptr_t dst) {
-    DecGeom g;
-    const uint64_t q = L >> 2;
-    const uint32_t r = static_cast<uint32_t>(L & 3u);
-    g.body_units = (r == 0) ? (q ? q - 1 : 0) : q;
-    g.nb = 3 * g.body_units;
-    g.h = static_cast<uint32_t>((4u - (dst & 3u)) & 3u);
-    g.nc = g.nb > g.h ? (g.nb - g.h) / 12 : 0;
-    g.u_first = g.h == 3 ? 1u : 0u;
-    return g;
-}
-
 // 6-bit value of each char; 0xFF for anything outside the alphabet ('=' too).
 __device__ __forceinline__ void build_dec_lut(uint8_t* lut) {
     for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x) {
@@ -256,6 +232,75 @@ __device__ __forceinline__ uint32_t dec_unit_bytes(const uint8_t* __restrict__ l
     return (d0 << 18) | (d1 << 12) | (d2 << 6) | d3;
 }
 
+// Tail item of one message: validates the body units no main item owns,
+// decodes the final unit, writes the head and tail bytes and sets status /
+// out_len (SN:281's IllegalArgumentException cases).
+__device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const StreamJob& job, const DecGeom& G,
+                                      const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                      int32_t* __restrict__ status, uint64_t* __restrict__ out_len) {
+    const uint64_t L = job.len;
+    uint32_t bad = 0;
+    const uint32_t r = static_cast<uint32_t>(L & 3u);
+    bool err = (r == 1u);
+    const uint64_t covered_end = G.u_first + 4 * G.ng;
+    for (uint64_t u = 0; u < G.body_units; ++u) {
+        if (u >= G.u_first && u < covered_end) { u = covered_end - 1; continue; }
+        dec_unit_bytes(lut, src, u, bad);
+    }
+    uint32_t fin_bytes = 0, fin_val = 0;
+    if (!err && L) {
+        const uint64_t f = 4 * G.body_units;  // first char of the final unit
+        if (r == 0) {
+            const uint32_t c2 = src[f + 2], c3 = src[f + 3];
+            const uint32_t d0 = dec_char(lut, src, f), d1 = dec_char(lut, src, f + 1);
+            const uint32_t d2 = lut[c2], d3 = lut[c3];
+            if ((d0 | d1) & 0x80u) err = true;
+            else if (c2 == '=' && c3 == '=') { fin_bytes = 1; fin_val = (d0 << 18) | (d1 << 12); }
+            else if (!(d2 & 0x80u) && c3 == '=') { fin_bytes = 2; fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6); }
+            else if (!((d2 | d3) & 0x80u)) { fin_bytes = 3; fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6) | d3; }
+            else err = true;
+        } else {  // r == 2 or 3: unpadded final unit
+            const uint32_t d0 = dec_char(lut, src, f), d1 = dec_char(lut, src, f + 1);
+            const uint32_t d2 = r == 3 ? dec_char(lut, src, f + 2) : 0u;
+            if ((d0 | d1 | d2) & 0x80u) err = true;
+            fin_bytes = r - 1;
+            fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6);
+        }
+    }
+    if (bad & 0x80u) err = true;
+    const uint64_t total = err ? 0 : G.nb + fin_bytes;
+    if (!err) {
+        // Head bytes [0, min(h, nb)) and tail bytes [h + 12nc, total).
+        auto byte_at = [&](uint64_t i) -> uint8_t {
+            const uint64_t u = i / 3;
+            uint32_t b2 = 0;
+            const uint32_t v = (u < G.body_units) ? dec_unit_bytes(lut, src, u, b2) : fin_val;
+            return static_cast<uint8_t>(v >> (16 - 8 * static_cast<uint32_t>(i % 3)));
+        };
+        const uint64_t head_end = G.h < total ? G.h : total;
+        for (uint64_t i = 0; i < head_end; ++i) dst[i] = byte_at(i);
+        for (uint64_t i = G.h + 16 * G.nchunks; i < total; ++i) {
+            if (i < head_end) continue;
+            dst[i] = byte_at(i);
+        }
+    }
+    int32_t flags = err ? 1 : 0;
+    if (job.expect && !err && total + 1 != job.expect) flags |= 2;
+    if (flags) atomicOr(status + job.id, flags);
+    if (out_len) out_len[job.id] = total;
+}
+
+// One tile = kDecGroupsPerTile 4-unit groups (16 KiB of chars) -> 12 KiB of
+// output.  Phase 1: lane l loads groups 256i + l (i < 4) with one dwordx4
+// each (a wave reads 1 KiB contiguous per instruction, all four loads in
+// flight), decodes them through the LDS alphabet and parks the 12 bytes of
+// each at LDS offset 12 * group.  Phase 2: lane l cuts 16-byte output chunks
+// 256i + l (i < 3) out of the decoded stream at byte offset e and writes
+// each with one dwordx4 store at a 16-byte aligned address (a wave writes
+// 1 KiB contiguous per instruction).  Head, tail and final unit: dec_tail,
+// on one lane of the message's last tile.  NT bit 0 = non-temporal stores,
+// bit 1 = non-temporal loads.
+template <int NT>
 __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
@@ -263,6 +308,7 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
                                                                   int32_t* __restrict__ status,
                                                                   uint64_t* __restrict__ out_len) {
     __shared__ uint8_t lut[256];
+    __shared__ uint32_t stream[kDecGroupsPerTile * 3 + 4];  // decoded bytes of the tile (+1 unit)
     build_dec_lut(lut);
     __syncthreads();
 
@@ -272,101 +318,68 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
     uint32_t j = find_job(jobs, njobs, t0);
     for (uint64_t t = t0; t < t1; ++t) {
         while (jobs[j + 1].tile_start <= t) ++j;
-        const uint64_t L = jobs[j].len;
         const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(in) + jobs[j].src_off;
         uint8_t* __restrict__ dst = out + jobs[j].dst_off;
-        const DecGeom G = dec_geom(L, reinterpret_cast<uintptr_t>(dst));
+        const DecGeom G = dec_geom(jobs[j].len, reinterpret_cast<uintptr_t>(dst));
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
-        const uint32_t id = jobs[j].id;
-        const uint64_t c0 = (t - jobs[j].tile_start) * kDecChunksPerTile + threadIdx.x;
-        const uint32_t e = G.h % 3u;                  // byte offset inside the first unit used
-        const bool five = (G.h == 1u || G.h == 2u);   // chunk straddles 5 units
+        const uint64_t k = t - jobs[j].tile_start;
+        const uint64_t g0 = k * kDecGroupsPerTile;  // first group of the tile
+        // Group g's chars start at unit u_first + 4g, i.e. dword w0 + 4g.
+        const uint32_t* w0 = reinterpret_cast<const uint32_t*>(src + 4 * G.u_first - sa);
+        uint32_t raw[4][5];
 #pragma unroll
-        for (int i = 0; i < kDecChunksPerTile / kStreamBlock; ++i) {
-            const uint64_t c = c0 + static_cast<uint64_t>(i) * kStreamBlock;
-            if (c < G.nc) {
-                const uint64_t U = 4 * c + G.u_first;  // first unit read
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + 4 * U - sa);
-                uint32_t raw[6];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) raw[k] = w[k];
-                raw[4] = (sa || five) ? w[4] : 0u;
-                raw[5] = (sa && five) ? w[5] : 0u;
-                uint32_t cw[5];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) cw[k] = align_bytes(raw[k + 1], raw[k], sa);
-                uint32_t bad = 0, bad5 = 0;
-                const uint32_t v0 = dec_unit(lut, cw[0], bad);
-                const uint32_t v1 = dec_unit(lut, cw[1], bad);
-                const uint32_t v2 = dec_unit(lut, cw[2], bad);
-                const uint32_t v3 = dec_unit(lut, cw[3], bad);
-                const uint32_t v4 = five ? dec_unit(lut, cw[4], bad5) : 0u;
-                if (bad & 0x80u) atomicOr(status + id, 1);
-                // 15 decoded bytes as LE words, then shift by e bytes.
-                const uint32_t x0 = __builtin_amdgcn_perm(v1, v0, 0x06000102u);
-                const uint32_t x1 = __builtin_amdgcn_perm(v2, v1, 0x05060001u);
-                const uint32_t x2 = __builtin_amdgcn_perm(v3, v2, 0x04050600u);
-                const uint32_t x3 = __builtin_amdgcn_perm(0u, v4, 0x0c000102u);
-                uint32_t* o = reinterpret_cast<uint32_t*>(dst + G.h + 12 * c);
-                o[0] = align_bytes(x1, x0, e);
-                o[1] = align_bytes(x2, x1, e);
-                o[2] = align_bytes(x3, x2, e);
-            } else if (c == G.nc) {
-                // ---- tail item ----
-                uint32_t bad = 0;
-                const uint32_t r = static_cast<uint32_t>(L & 3u);
-                bool err = (r == 1u);
-                // Body units no main item validated.
-                const uint64_t covered_end = G.u_first + 4 * G.nc;
-                for (uint64_t u = 0; u < G.body_units; ++u) {
-                    if (u >= G.u_first && u < covered_end) { u = covered_end - 1; continue; }
-                    dec_unit_bytes(lut, src, u, bad);
-                }
-                // Final unit.
-                uint32_t fin_bytes = 0, fin_val = 0;
-                if (!err && L) {
-                    const uint64_t f = 4 * G.body_units;  // first char of the final unit
-                    if (r == 0) {
-                        const uint32_t c2 = src[f + 2], c3 = src[f + 3];
-                        const uint32_t d0 = dec_char(lut, src, f), d1 = dec_char(lut, src, f + 1);
-                        const uint32_t d2 = lut[c2], d3 = lut[c3];
-                        if ((d0 | d1) & 0x80u) err = true;
-                        else if (c2 == '=' && c3 == '=') { fin_bytes = 1; fin_val = (d0 << 18) | (d1 << 12); }
-                        else if (!(d2 & 0x80u) && c3 == '=') { fin_bytes = 2; fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6); }
-                        else if (!((d2 | d3) & 0x80u)) { fin_bytes = 3; fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6) | d3; }
-                        else err = true;
-                    } else {  // r == 2 or 3: unpadded final unit
-                        const uint32_t d0 = dec_char(lut, src, f), d1 = dec_char(lut, src, f + 1);
-                        const uint32_t d2 = r == 3 ? dec_char(lut, src, f + 2) : 0u;
-                        if ((d0 | d1 | d2) & 0x80u) err = true;
-                        fin_bytes = r - 1;
-                        fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6);
-                    }
-                }
-                if (bad & 0x80u) err = true;
-                const uint64_t total = err ? 0 : G.nb + fin_bytes;
-                if (!err) {
-                    // Head bytes [0, min(h, nb)) and tail bytes [h + 12nc, total).
-                    auto byte_at = [&](uint64_t i) -> uint8_t {
-                        const uint64_t u = i / 3;
-                        uint32_t b2 = 0;
-                        const uint32_t v = (u < G.body_units) ? dec_unit_bytes(lut, src, u, b2) : fin_val;
-                        return static_cast<uint8_t>(v >> (16 - 8 * static_cast<uint32_t>(i % 3)));
-                    };
-                    const uint64_t head_end = G.h < total ? G.h : total;
-                    for (uint64_t i = 0; i < head_end; ++i) dst[i] = byte_at(i);
-                    for (uint64_t i = G.h + 12 * G.nc; i < total; ++i) {
-                        if (i < head_end) continue;
-                        dst[i] = byte_at(i);
-                    }
-                }
-                const uint64_t expect = jobs[j].expect;
-                int32_t flags = err ? 1 : 0;
-                if (expect && !err && total + 1 != expect) flags |= 2;
-                if (flags) atomicOr(status + id, flags);
-                if (out_len) out_len[id] = total;
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t g = g0 + threadIdx.x + static_cast<uint64_t>(i) * kStreamBlock;
+            raw[i][0] = raw[i][1] = raw[i][2] = raw[i][3] = raw[i][4] = 0u;
+            if (g < G.ng) {
+                const uint32_t* w = w0 + 4 * g;
+                u32x4 v;
+                if (NT & 2) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
+                else v = *reinterpret_cast<const u32x4*>(w);
+                raw[i][0] = v.x; raw[i][1] = v.y; raw[i][2] = v.z; raw[i][3] = v.w;
+                if (sa) raw[i][4] = (NT & 2) ? __builtin_nontemporal_load(w + 4) : w[4];
             }
         }
+        uint32_t bad = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t gl = threadIdx.x + static_cast<uint32_t>(i) * kStreamBlock;  // group in the tile
+            if (g0 + gl < G.ng) {
+                uint32_t v[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = dec_unit(lut, align_bytes(raw[i][q + 1], raw[i][q], sa), bad);
+                stream[3 * gl] = __builtin_amdgcn_perm(v[1], v[0], 0x06000102u);
+                stream[3 * gl + 1] = __builtin_amdgcn_perm(v[2], v[1], 0x05060001u);
+                stream[3 * gl + 2] = __builtin_amdgcn_perm(v[3], v[2], 0x04050600u);
+            }
+        }
+        // The tile's last chunk reaches e bytes into the next group's first
+        // unit (a body unit whenever that chunk exists); its chars are
+        // validated by the tile that owns it.
+        const uint64_t c0 = k * kDecChunksPerTile;  // first chunk of the tile
+        if (threadIdx.x == 0 && G.e && c0 + kDecChunksPerTile <= G.nchunks) {
+            uint32_t b2 = 0;
+            const uint32_t v = dec_unit_bytes(lut, src, G.u_first + 4 * (g0 + kDecGroupsPerTile), b2);
+            stream[3 * kDecGroupsPerTile] = __builtin_amdgcn_perm(0u, v, 0x0c000102u);
+        }
+        if (bad & 0x80u) atomicOr(status + jobs[j].id, 1);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t m = threadIdx.x + static_cast<uint32_t>(i) * kStreamBlock;  // chunk in the tile
+            if (c0 + m < G.nchunks) {
+                const u32x4 a = *reinterpret_cast<const u32x4*>(stream + 4 * m);
+                const uint32_t n4 = G.e ? stream[4 * m + 4] : 0u;
+                const u32x4 o = u32x4{align_bytes(a.y, a.x, G.e), align_bytes(a.z, a.y, G.e),
+                                      align_bytes(a.w, a.z, G.e), align_bytes(n4, a.w, G.e)};
+                u32x4* d = reinterpret_cast<u32x4*>(dst + G.h + 16 * (c0 + m));
+                if (NT & 1) __builtin_nontemporal_store(o, d);
+                else *d = o;
+            }
+        }
+        if (threadIdx.x == 0 && t + 1 == jobs[j + 1].tile_start)  // the message's last tile
+            dec_tail(lut, jobs[j], G, src, dst, status, out_len);
+        __syncthreads();  // stream[] is rewritten by the next tile
     }
 }
 
@@ -395,10 +408,17 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 }
 
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                             int32_t* status, uint64_t* out_len, hipStream_t s) {
+                             int32_t* status, uint64_t* out_len, hipStream_t s, int nt) {
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(b64_decode_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, in, jobs, njobs,
-                       ntiles, out, status, out_len);
+    const dim3 g(stream_grid(ntiles)), b(kStreamBlock);
+#define DFS_DEC(N) hipLaunchKernelGGL((b64_decode_kernel<N>), g, b, 0, s, in, jobs, njobs, ntiles, out, status, out_len)
+    switch (nt & 3) {
+        case 0: DFS_DEC(0); break;
+        case 1: DFS_DEC(1); break;
+        case 2: DFS_DEC(2); break;
+        default: DFS_DEC(3); break;
+    }
+#undef DFS_DEC
     return hipGetLastError();
 }
 

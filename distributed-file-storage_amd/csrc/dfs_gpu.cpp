@@ -67,6 +67,7 @@ struct dfs_ctx {
     int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
     int b64_nt = 3;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
+    int dec_nt = 3;              // non-temporal decode: bit 0 stores, bit 1 loads (DFS_DEC_NT)
     bool b64_pair = true;        // 12-bit pair table (DFS_B64_LUT=12) vs 6-bit alphabet (=6)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
@@ -147,15 +148,11 @@ uint64_t finish_jobs(std::vector<StreamJob>& jobs, const std::vector<uint64_t>& 
     return t;
 }
 
-// Decode geometry (must match dec_geom in base64.hip): items = nc + 1.
+// Decode work of one message in 4-unit groups (dfs::dec_geom); at least one
+// tile, whose last one also runs the tail step.
 uint64_t dec_items(uint64_t L, uintptr_t dst) {
-    const uint64_t q = L >> 2;
-    const uint32_t r = static_cast<uint32_t>(L & 3u);
-    const uint64_t body_units = (r == 0) ? (q ? q - 1 : 0) : q;
-    const uint64_t nb = 3 * body_units;
-    const uint32_t h = static_cast<uint32_t>((4u - (dst & 3u)) & 3u);
-    const uint64_t nc = nb > h ? (nb - h) / 12 : 0;
-    return nc + 1;
+    const uint64_t ng = dfs::dec_geom(L, dst).ng;
+    return ng ? ng : 1;
 }
 
 uint64_t copy_items(uint64_t len, uintptr_t dst) {
@@ -230,6 +227,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
     if (const char* w = std::getenv("DFS_B64_NT")) c->b64_nt = std::atoi(w) & 3;
+    if (const char* w = std::getenv("DFS_DEC_NT")) c->dec_nt = std::atoi(w) & 3;
     if (const char* w = std::getenv("DFS_B64_LUT")) c->b64_pair = std::atoi(w) != 6;
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     hipError_t e = hipSetDevice(device);
@@ -561,7 +559,7 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
         j.id = i;
         items[i] = dec_items(msgs[i].len, reinterpret_cast<uintptr_t>(d_out + out_off[i]));
     }
-    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecChunksPerTile);
+    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecGroupsPerTile);
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * n));
     HIPC(c->buf[B_OUTLEN].ensure(8ull * n));
@@ -569,7 +567,8 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64DEC, s);
     HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), n, ntiles, d_out,
-                                c->buf[B_STATUS].as<int32_t>(), c->buf[B_OUTLEN].as<uint64_t>(), s));
+                                c->buf[B_STATUS].as<int32_t>(), c->buf[B_OUTLEN].as<uint64_t>(), s,
+                                c->dec_nt));
     tm.end(DFS_T_B64DEC, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(n);
@@ -991,7 +990,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         sha.push_back(msg(file_off[f], file_len[f], nf + f));
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecChunksPerTile);
+    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecGroupsPerTile);
     const uint32_t prio = sort_lanes(sha);  // one message per lane, persistent sha256_lanes
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
@@ -1002,7 +1001,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64DEC, s);
     HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out,
-                                c->buf[B_STATUS].as<int32_t>(), nullptr, s));
+                                c->buf[B_STATUS].as<int32_t>(), nullptr, s, c->dec_nt));
     tm.end(DFS_T_B64DEC, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));

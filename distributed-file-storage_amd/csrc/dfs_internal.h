@@ -44,8 +44,39 @@ constexpr int kShaBlock = 256;       // threads per SHA workgroup (4 waves)
 constexpr size_t kShaQueueBytes = 4 * (64 + 8192);  // SHA queue words + per-SIMD tokens
 constexpr int kStreamBlock = 256;    // threads per stream workgroup
 constexpr int kEncGroupsPerTile = 1024;  // 12-byte groups (4 per thread)
-constexpr int kDecChunksPerTile = 1024;  // 12-byte output chunks (4 per thread)
-constexpr int kCopyChunksPerTile = 1024; // 16-byte output chunks (4 per thread)
+// Base64 decode geometry of one message of L chars decoding to dst (shared
+// by the host's tile count and b64_decode_kernel).  q = L/4 full units, r =
+// L%4; the final unit (padded, or the r trailing chars) is decoded by the
+// tail step, the body_units before it by tiles of kDecGroupsPerTile 4-unit
+// groups starting at unit u_first = h/3, where h = bytes up to the first
+// 16-byte aligned output address.  Main output = 16-byte chunks
+// [h + 16m, h + 16m + 16), m < nchunks, cut from the decoded stream of the
+// ng whole groups at byte offset e = h % 3.
+constexpr int kDecGroupsPerTile = 4 * kStreamBlock;  // 4 groups per thread
+constexpr int kDecChunksPerTile = 3 * kStreamBlock;  // 16-byte output chunks (3 per thread)
+constexpr int kCopyChunksPerTile = 1024; // gather: 16-byte output chunks (4 per thread)
+struct DecGeom {
+    uint64_t body_units;
+    uint64_t nb;       // body bytes
+    uint32_t h;        // head bytes
+    uint32_t u_first;  // first unit of group 0
+    uint32_t e;        // h % 3
+    uint64_t ng;       // whole 4-unit groups decoded by the tiles
+    uint64_t nchunks;  // 16-byte output chunks written by the tiles
+};
+__host__ __device__ inline DecGeom dec_geom(uint64_t L, uintptr_t dst) {
+    DecGeom g;
+    const uint64_t q = L >> 2;
+    const uint32_t r = static_cast<uint32_t>(L & 3u);
+    g.body_units = (r == 0) ? (q ? q - 1 : 0) : q;
+    g.nb = 3 * g.body_units;
+    g.h = static_cast<uint32_t>((16u - (dst & 15u)) & 15u);
+    g.u_first = g.h / 3u;
+    g.e = g.h % 3u;
+    g.ng = g.body_units > g.u_first ? (g.body_units - g.u_first) / 4 : 0;
+    g.nchunks = 12 * g.ng > g.e ? (12 * g.ng - g.e) / 16 : 0;
+    return g;
+}
 
 // Tiles per job.
 inline uint64_t enc_tiles(uint64_t len) {
@@ -70,9 +101,10 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 // Decode: chars of job j at in + src_off decode to out + dst_off.
 // status[id] |= 1 on an IllegalArgumentException case; out_len[id] = bytes.
 // If job.expect != 0 it is the expected decoded length + 1 (download path):
-// a different length sets status bit 2.
+// a different length sets status bit 2.  nt bit 0 = non-temporal stores,
+// bit 1 = non-temporal loads.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s);
+                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, int nt = 3);
 // Gather: job.src_off is an absolute device address of the fragment.
 hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
                          hipStream_t s);
