@@ -226,16 +226,41 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
         ok = ok and bool((st == 0).all())
     eng.set_profiling(False)
     ok = ok and bool(torch.equal(out, files[:F * S]))
+    # Raw-fragment reassembly (SN:419-451, fragments fetched as raw bytes,
+    # :513-514): gather the fragments of every file (spans of the upload
+    # buffer) into `out`, then the fileId re-verify (:454-458).
+    from dfs_amd.engine import reassemble_device
+    out.zero_()
+    lens = np.array(split(S, N), dtype=np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    addr = (np.uint64(files.data_ptr()) + file_off[:, None] + offs[None, :]).reshape(-1)
+    flen = np.tile(lens, F)
+    exp = fd[:F * 32].cpu().numpy().reshape(F, 32)
+    reassemble_device(eng, addr, flen, F, N, out.data_ptr(), file_off, exp)
+    torch.cuda.synchronize(dev)
+    eng.set_profiling(True)
+    gat = []
+    for _ in range(reps):
+        st, _dig = reassemble_device(eng, addr, flen, F, N, out.data_ptr(), file_off, exp)
+        gat.append(eng.timings()["gather"])
+        ok = ok and bool((st == 0).all())
+    eng.set_profiling(False)
+    ok = ok and bool(torch.equal(out, files[:F * S]))
     del out
+    gat_ms = float(np.mean(gat))
+    gat_gbs = 2 * F * S / (gat_ms / 1e3) / 1e9
     dev_ms = float(np.mean(tot))
     dec_ms = float(np.mean(dec))
     dec_bytes = int(msp[:, 1].sum()) + F * S  # Base64 read + bytes written
-    log(f"download: {F} files, device {dev_ms:.1f} ms (decode {dec_ms:.1f}, sha {np.mean(sha):.1f}), ok={ok}")
+    log(f"download: {F} files, device {dev_ms:.1f} ms (decode {dec_ms:.1f}, sha {np.mean(sha):.1f}), "
+        f"raw gather {gat_ms:.1f} ms, ok={ok}")
     return {"files_per_gpu": F, "device_ms": round(dev_ms, 3), "wall_ms": round(float(np.mean(wall)) * 1e3, 3),
             "gbps": round(F * S / (dev_ms / 1e3) / 1e9, 2),
             "decode_ms": round(dec_ms, 3), "decode_gbs": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
             "decode_frac_hbm": round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-            "sha_ms": round(float(np.mean(sha)), 3), "ok": ok,
+            "sha_ms": round(float(np.mean(sha)), 3),
+            "gather_ms": round(gat_ms, 3), "gather_gbs": round(gat_gbs, 1),
+            "gather_frac_hbm": round(gat_gbs / HBM_PEAK_GBS, 4), "ok": ok,
             "note": "wall_ms includes host-side job planning per call; gbps = file bytes / device time"}
 
 

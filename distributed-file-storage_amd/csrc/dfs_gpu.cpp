@@ -155,9 +155,11 @@ uint64_t dec_items(uint64_t L, uintptr_t dst) {
     return ng ? ng : 1;
 }
 
+// Gather items of one fragment (must match gather_kernel): 16-byte chunks
+// from the first 16-aligned destination address + one head/tail item.
 uint64_t copy_items(uint64_t len, uintptr_t dst) {
     if (!len) return 0;
-    const uint32_t h = static_cast<uint32_t>((4u - (dst & 3u)) & 3u);
+    const uint32_t h = static_cast<uint32_t>((16u - (dst & 15u)) & 15u);
     const uint64_t nc = len > h ? (len - h) / 16 : 0;
     return nc + 1;
 }

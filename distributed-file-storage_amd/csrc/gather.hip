@@ -3,15 +3,26 @@
 // gather_kernel replaces handleDownload's ordered reassembly
 // (ByteArrayOutputStream.write at StorageNode.java:448, toByteArray at :451):
 // fragment i of file f is copied to file_off[f] + off_i (the split offsets
-// of :138-157).  HBM-bound: every destination dword is written once by an
-// aligned store; misaligned sources are funnel-shifted in registers.
+// of :138-157).  HBM-bound: every destination byte is written once, by
+// 16-byte aligned stores; misaligned sources are funnel-shifted in registers.
 #include "stream_common.h"
 
 namespace dfs {
 namespace {
 
+// Tile = kCopyChunksPerTile 16-byte output chunks: chunk c of a fragment
+// covers dst bytes [h + 16c, h + 16c + 16), a 16-byte aligned span (h = bytes
+// up to the first 16-aligned address, copy_items in dfs_gpu.cpp).  Every lane
+// issues the loads of all its chunks (dwordx4 + one dword when the source is
+// not dword-aligned relative to the destination) before any store; a wave
+// reads and writes 1 KiB contiguous per instruction.  One lane per fragment
+// copies the head and tail bytes.  Loads and stores are non-temporal: every
+// byte is touched once.
+typedef uint32_t g32x4 __attribute__((ext_vector_type(4)));
+
 __global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* __restrict__ jobs, uint32_t njobs,
                                                               uint64_t ntiles, uint8_t* __restrict__ out) {
+    constexpr int P = kCopyChunksPerTile / kStreamBlock;
     uint64_t t0, t1;
     tile_range(ntiles, t0, t1);
     if (t0 >= t1) return;
@@ -21,27 +32,35 @@ __global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* _
         const uint64_t len = jobs[j].len;
         const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(jobs[j].src_off);
         uint8_t* __restrict__ dst = out + jobs[j].dst_off;
-        const uint32_t h = static_cast<uint32_t>((4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u);
+        const uint32_t h = static_cast<uint32_t>((16u - (reinterpret_cast<uintptr_t>(dst) & 15u)) & 15u);
         const uint64_t nc = len > h ? (len - h) / 16 : 0;
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src + h)) & 3u;
+        const uint32_t* w0 = reinterpret_cast<const uint32_t*>(src + h - sa);
         const uint64_t c0 = (t - jobs[j].tile_start) * kCopyChunksPerTile + threadIdx.x;
+        g32x4 v[P];
+        uint32_t x[P];
 #pragma unroll
-        for (int i = 0; i < kCopyChunksPerTile / kStreamBlock; ++i) {
+        for (int i = 0; i < P; ++i) {
+            const uint64_t c = c0 + static_cast<uint64_t>(i) * kStreamBlock;
+            v[i] = g32x4{0u, 0u, 0u, 0u};
+            x[i] = 0u;
+            if (c < nc) {
+                v[i] = __builtin_nontemporal_load(reinterpret_cast<const g32x4*>(w0 + 4 * c));
+                if (sa) x[i] = __builtin_nontemporal_load(w0 + 4 * c + 4);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
             const uint64_t c = c0 + static_cast<uint64_t>(i) * kStreamBlock;
             if (c < nc) {
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(src + h + 16 * c - sa);
-                const uint4 v = *reinterpret_cast<const uint4*>(w);
-                uint4 o;
+                g32x4 o = v[i];
                 if (sa) {
-                    const uint32_t x = w[4];
-                    o.x = __builtin_amdgcn_alignbyte(v.y, v.x, sa);
-                    o.y = __builtin_amdgcn_alignbyte(v.z, v.y, sa);
-                    o.z = __builtin_amdgcn_alignbyte(v.w, v.z, sa);
-                    o.w = __builtin_amdgcn_alignbyte(x, v.w, sa);
-                } else {
-                    o = v;
+                    o.x = __builtin_amdgcn_alignbyte(v[i].y, v[i].x, sa);
+                    o.y = __builtin_amdgcn_alignbyte(v[i].z, v[i].y, sa);
+                    o.z = __builtin_amdgcn_alignbyte(v[i].w, v[i].z, sa);
+                    o.w = __builtin_amdgcn_alignbyte(x[i], v[i].w, sa);
                 }
-                *reinterpret_cast<uint4*>(dst + h + 16 * c) = o;
+                __builtin_nontemporal_store(o, reinterpret_cast<g32x4*>(dst + h + 16 * c));
             } else if (c == nc) {
                 const uint64_t head_end = h < len ? h : len;
                 for (uint64_t b = 0; b < head_end; ++b) dst[b] = src[b];

@@ -353,6 +353,27 @@ def download_device(engine: "FragmentEngine", d_b64: int, spans: np.ndarray, nfi
     return status[:nfiles]
 
 
+def reassemble_device(engine: "FragmentEngine", frag_addr: np.ndarray, frag_len: np.ndarray, nfiles: int,
+                      nfrag: int, d_out: int, file_off: np.ndarray,
+                      expected: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """dfs_reassemble_verify with device fragments and output (raw-fragment
+    download, SN:419-458): frag_addr[k] = device address of fragment k (0 =
+    missing); expected = host (nfiles, 32) fileId digests or None.  Returns
+    (per-file status, (nfiles, 32) digests of the rebuilt files)."""
+    addr = np.ascontiguousarray(frag_addr, dtype=np.uint64)
+    frag_len = np.ascontiguousarray(frag_len, dtype=np.uint64)
+    file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
+    exp = None if expected is None else np.ascontiguousarray(expected, dtype=np.uint8)
+    status = np.zeros(max(nfiles, 1), dtype=np.int32)
+    dig = np.zeros((max(nfiles, 1), 32), dtype=np.uint8)
+    rc = lib().dfs_reassemble_verify(engine.ctx, _ptr(addr), _ptr(frag_len), nfiles, nfrag, ctypes.c_void_p(d_out),
+                                    _ptr(file_off), _ptr(exp) if exp is not None else None, _ptr(dig),
+                                    _ptr(status), L.DFS_DEVICE_PTRS)
+    if rc not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_CORRUPT):
+        check(rc, "dfs_reassemble_verify")
+    return status[:nfiles], dig[:nfiles]
+
+
 class UploadPlan:
     """dfs_upload_plan over device-resident (torch) buffers — the bench path."""
 

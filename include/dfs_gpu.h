@@ -180,7 +180,9 @@ int dfs_upload_batch(dfs_ctx* ctx, const uint8_t* files, const dfs_span* file_sp
  * in index order, SN:448); file_digest_out[f] = SHA-256(rebuilt file) (SN:454)
  * and status[f] = 0, DFS_E_MISSING (a NULL source, SN:443-446) or
  * DFS_E_CORRUPT (digest != expected_file_digest[f], SN:455-458).
- * expected_file_digest may be NULL (status then only reports MISSING). */
+ * expected_file_digest may be NULL (status then only reports MISSING);
+ * expected_file_digest, file_digest_out and status are host memory in every
+ * mode (DFS_DEVICE_PTRS covers frag_src and out). */
 int dfs_reassemble_verify(dfs_ctx* ctx, const uint8_t* const* frag_src, const uint64_t* frag_len,
                           uint32_t nfiles, uint32_t nfrag, uint8_t* out, const uint64_t* file_off,
                           const uint8_t* expected_file_digest, uint8_t* file_digest_out,
