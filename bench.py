@@ -343,8 +343,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # A stuck exchange in the side legs must raise (and be reported in the
+        # JSON line) rather than hang or abort the job: blocking waits with a
+        # bounded timeout, communicator cleanup without process teardown.
+        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+        import datetime
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=240))
     dev = torch.device("cuda", local if world > 1 else 0)
 
     def log(msg):

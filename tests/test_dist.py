@@ -1,4 +1,5 @@
-"""Multi-rank placement (gloo on CPU, world 2 and 4).
+"""Multi-rank placement (gloo on CPU, world 2, 4 and 8; 8 ranks x 5 nodes is
+the bench's 8-GPU replication leg, GPUs 5-7 hosting no node).
 
 Checks that the replication exchange leaves every rank holding exactly the
 fragments of the nodes it hosts (node k stores {k, k+1}, SN:143-145,
@@ -80,7 +81,8 @@ def _worker(rank, world, port, nfrag, nfiles, offline, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,nfrag,offline", [(2, 5, ()), (2, 5, (1,)), (4, 4, ()), (4, 4, (2,)), (4, 8, (0,))])
+@pytest.mark.parametrize("world,nfrag,offline", [(2, 5, ()), (2, 5, (1,)), (4, 4, ()), (4, 4, (2,)), (4, 8, (0,)),
+                                                       (4, 3, (3,)), (8, 5, (7,))])
 def test_placement_exchange(world, nfrag, offline):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
