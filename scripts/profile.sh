@@ -21,3 +21,19 @@ for ctr in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
     python3 bench.py $ARGS > gpurun_out/prof_pmc/p$i.json 2> gpurun_out/prof_pmc/p$i.err || fatal $?
 done
 python3 tools/pmc_summary.py gpurun_out gpurun_out/pmc_summary.json "${WORKLOAD_TAG:-65536x1048576/N5}"
+# Download leg (Base64 decode into place, raw-fragment gather): its own kernel
+# trace and HBM passes, one upload step first to produce the Base64.
+[ -n "${NO_DL_PROF}" ] && exit 0
+DLARGS="--steps 1 --warmup 0 --b64-steps 1 --dl-steps 3 --no-cpu-baseline --verify 0 --serial ${PROF_ARGS}"
+mkdir -p gpurun_out/prof_dl
+echo "== download kernel trace"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dl/trace -o trace --output-format csv -- \
+  python3 bench.py $DLARGS > gpurun_out/prof_dl/bench.json 2> gpurun_out/prof_dl/bench.err || fatal $?
+i=0
+for ctr in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  echo "== download pmc pass $i: $ctr"
+  timeout -s KILL 300 rocprofv3 --pmc $ctr -d gpurun_out/prof_dl/p$i -o pmc --output-format csv -- \
+    python3 bench.py $DLARGS > gpurun_out/prof_dl/p$i.json 2> gpurun_out/prof_dl/p$i.err || fatal $?
+done
+python3 tools/pmc_summary.py gpurun_out/prof_dl gpurun_out/pmc_download_summary.json "${WORKLOAD_TAG:-65536x1048576/N5} download"
