@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--rep-steps", type=int, default=3)
     ap.add_argument("--no-download", action="store_true", help="skip the download/verify leg")
     ap.add_argument("--dl-steps", type=int, default=2)
+    ap.add_argument("--wire-files", type=int, default=16384, help="files in the storeFragments body leg")
+    ap.add_argument("--no-wire", action="store_true", help="skip the storeFragments body leg")
     ap.add_argument("--config", type=int, default=2, choices=(2, 4),
                     help="2: BASELINE configs[1] (default bench line); 4: configs[3], the long-fragment skew "
                          "(1,024 x 256 MiB, N=5) streamed through HBM in chunks, its own JSON line")
@@ -262,6 +264,63 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
             "gather_ms": round(gat_ms, 3), "gather_gbs": round(gat_gbs, 1),
             "gather_frac_hbm": round(gat_gbs / HBM_PEAK_GBS, 4), "ok": ok,
             "note": "wall_ms includes host-side job planning per call; gbps = file bytes / device time"}
+
+
+def wire_leg(args, eng, files, fd, S, N, F, dev, log):
+    """storeFragments request bodies on the device (SN:195-205 + 629-642):
+    node 1 (0-based 0) uploads; for each sampled file the N-1 peer bodies
+    {"fileId":..,"fragments":[{k},{k+1}]} with the Base64 encoded straight
+    from the file bytes into the body.  Timed with HIP events; the first and
+    last files are checked byte-for-byte against the oracle's
+    buildFragmentsJson.  Returns a dict for the JSON line."""
+    import numpy as np
+    import torch
+    from dfs_amd.engine import store_bodies_layout, store_bodies_device
+    R = min(F, args.wire_files)
+    spans = np.stack([np.arange(R, dtype=np.uint64) * np.uint64(S), np.full(R, S, dtype=np.uint64)], axis=1)
+    body_off = store_bodies_layout(eng, spans, N, 0)
+    bodies = torch.empty(int(body_off[-1]) + 16, dtype=torch.uint8, device=dev)
+
+    def once():
+        store_bodies_device(eng, files.data_ptr(), spans, N, 0, fd.data_ptr(), bodies.data_ptr(), body_off)
+
+    once()
+    torch.cuda.synchronize(dev)
+    eng.set_profiling(True)
+    tot, enc = [], []
+    for _ in range(max(1, args.dl_steps)):
+        once()
+        t = eng.timings()
+        tot.append(t["total"]); enc.append(t["b64enc"])
+    eng.set_profiling(False)
+    torch.cuda.synchronize(dev)
+    ok = True
+    if args.verify:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import hashlib
+        import oracle as O  # checker only
+        host = None
+        for f in sorted({0, R - 1}):
+            data = files[f * S:(f + 1) * S].cpu().numpy().tobytes()
+            fid = hashlib.sha256(data).hexdigest()
+            parts = [data[o:o + n] for o, n in O.py_split(S, N)]
+            for j, k in enumerate(range(1, N)):
+                want = O.py_build_fragments_json(fid, [(k, parts[k]), (((k + 1) % N), parts[(k + 1) % N])]).encode()
+                o = int(body_off[f * (N - 1) + j])
+                ok &= bodies[o:o + len(want)].cpu().numpy().tobytes() == want
+    lens = split(S, N)
+    body_bytes = sum(139 + 4 * ((lens[k] + 2) // 3) + 4 * ((lens[(k + 1) % N] + 2) // 3) for k in range(1, N))
+    raw_read = sum(lens[k] + lens[(k + 1) % N] for k in range(1, N))
+    moved = R * (body_bytes + raw_read)
+    ms = float(np.mean(tot))
+    log(f"wire: {R} files x {N - 1} storeFragments bodies, {ms:.1f} ms, ok={ok}")
+    del bodies
+    return {"files": R, "bodies": R * (N - 1), "uploader_node": 1, "ms": round(ms, 3),
+            "encode_ms": round(float(np.mean(enc)), 3), "body_gbs": round(R * body_bytes / (ms / 1e3) / 1e9, 1),
+            "hbm_gbs": round(moved / (ms / 1e3) / 1e9, 1), "hbm_frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "ok": bool(ok),
+            "note": "bodies byte-identical to buildFragmentsJson (SN:629-642); hbm_gbs = raw fragment bytes read "
+                    "+ body bytes written per second"}
 
 
 def long_leg(args):
@@ -486,6 +545,11 @@ def main():
             result["download"] = download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log)
         except Exception as e:
             result["download"] = {"error": repr(e)[:300]}
+    if not args.no_wire:
+        try:
+            result["wire"] = wire_leg(args, eng, files, fd, S, N, F, dev, log)
+        except Exception as e:
+            result["wire"] = {"error": repr(e)[:300]}
     if world > 1 and not args.no_replicate:
         try:
             result["replication"] = replication_leg(args, eng, files, S, N, dev, log)

@@ -423,3 +423,64 @@ hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njo
 }
 
 }  // namespace dfs
+
+// ---------------------------------------------------------------------------
+// storeFragments body framing (buildFragmentsJson, StorageNode.java:629-642):
+//   {"fileId":"<64 hex>","fragments":[{"index":"a","data":"<B1 chars>"},
+//    {"index":"b","data":"<B2 chars>"}]}
+// 139 framing bytes around two Base64 payloads (written by the encode
+// kernel at body + 111 and body + 135 + B1).  One thread per framing byte.
+// ---------------------------------------------------------------------------
+namespace dfs {
+namespace {
+
+__constant__ char kBodyPrefix[] = "{\"fileId\":\"0123456789012345678901234567890123456789012345678901234567890123"
+                                  "\",\"fragments\":[{\"index\":\"0\",\"data\":\"";
+__constant__ char kBodyMid[] = "\"},{\"index\":\"0\",\"data\":\"";
+__constant__ char kBodySuffix[] = "\"}]}";
+
+__global__ __launch_bounds__(256) void store_body_frame_kernel(const StoreBody* __restrict__ bodies, uint32_t n,
+                                                               const uint8_t* __restrict__ digests,
+                                                               char* __restrict__ out) {
+    const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t k = g / kBodyFrameBytes;
+    if (k >= n) return;
+    const uint32_t p = static_cast<uint32_t>(g - k * kBodyFrameBytes);
+    const StoreBody B = bodies[k];
+    char c;
+    uint64_t at;
+    if (p < kBodyDataA) {
+        at = p;
+        if (p >= 11 && p < 75) {  // fileId hex, lowercase %02x (SN:607-609)
+            const uint32_t byte = digests[32ull * B.file + (p - 11) / 2];
+            const uint32_t nib = (p & 1u) ? (byte >> 4) : (byte & 15u);  // p = 11 -> high nibble
+            c = static_cast<char>(nib < 10 ? '0' + nib : 'a' + nib - 10);
+        } else if (p == kBodyDataA - 11) {
+            c = static_cast<char>('0' + B.a);
+        } else {
+            c = kBodyPrefix[p];
+        }
+    } else if (p < kBodyDataA + kBodyMidBytes) {
+        const uint32_t q = p - kBodyDataA;
+        at = kBodyDataA + B.len_a + q;
+        c = (q == kBodyMidBytes - 11) ? static_cast<char>('0' + B.b) : kBodyMid[q];
+    } else {
+        const uint32_t q = p - kBodyDataA - kBodyMidBytes;
+        at = kBodyDataA + kBodyMidBytes + B.len_a + B.len_b + q;
+        c = kBodySuffix[q];
+    }
+    out[B.dst + at] = c;
+}
+
+}  // namespace
+
+hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
+                                   hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t threads = static_cast<uint64_t>(n) * kBodyFrameBytes;
+    hipLaunchKernelGGL(store_body_frame_kernel, dim3(static_cast<uint32_t>((threads + 255) / 256)), dim3(256), 0, s,
+                       bodies, n, digests, out);
+    return hipGetLastError();
+}
+
+}  // namespace dfs

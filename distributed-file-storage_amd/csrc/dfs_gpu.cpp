@@ -1079,4 +1079,97 @@ int dfs_synth_fill_at(dfs_ctx* c, uint8_t* d_dst, const dfs_span* files, uint32_
     return DFS_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// storeFragments wire codec, sender side: sendFragmentsToPeers (SN:195-205)
+// + buildFragmentsJson (SN:629-642) for a whole batch on the device.
+uint64_t dfs_store_body_len(uint64_t file_len, uint32_t nfrag, uint32_t a, uint32_t b) {
+    if (!nfrag || a >= nfrag || b >= nfrag) return 0;
+    std::vector<uint64_t> off(nfrag), len(nfrag);
+    split(file_len, nfrag, off.data(), len.data());
+    return dfs::kBodyFrameBytes + enc_len(len[a]) + enc_len(len[b]);
+}
+
+int dfs_store_bodies_build(dfs_ctx* c, const uint8_t* files, const dfs_span* file_spans, uint32_t nfiles,
+                           uint32_t nfrag, uint32_t uploader, const uint8_t* file_digest, char* bodies,
+                           uint64_t* body_off, uint32_t flags) {
+    if (!c || !body_off || nfrag < 2 || nfrag > 10 || uploader >= nfrag || (nfiles && !file_spans))
+        return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    const uint32_t peers = nfrag - 1;
+    std::vector<dfs::StoreBody> desc;
+    std::vector<StreamJob> jobs;
+    std::vector<uint64_t> items, off(nfrag), len(nfrag);
+    desc.reserve(static_cast<size_t>(nfiles) * peers);
+    uint64_t total = 0, end = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        split(file_spans[f].len, nfrag, off.data(), len.data());  // SN:138-157
+        end = std::max(end, file_spans[f].off + file_spans[f].len);
+        for (uint32_t k = 0, j = 0; k < nfrag; ++k) {
+            if (k == uploader) continue;  // SN:197
+            const uint32_t a = k, b = (k + 1) % nfrag;  // SN:199-200
+            dfs::StoreBody B{};
+            B.dst = total + dfs::kBodyStartPhase;
+            B.len_a = enc_len(len[a]);
+            B.len_b = enc_len(len[b]);
+            B.file = f;
+            B.a = static_cast<uint16_t>(a);
+            B.b = static_cast<uint16_t>(b);
+            desc.push_back(B);
+            const uint64_t dst2[2] = {B.dst + dfs::kBodyDataA, B.dst + dfs::kBodyDataA + dfs::kBodyMidBytes + B.len_a};
+            const uint32_t fr[2] = {a, b};
+            for (int q = 0; q < 2; ++q) {
+                if (!len[fr[q]]) continue;
+                StreamJob jb{};
+                jb.src_off = file_spans[f].off + off[fr[q]];
+                jb.len = len[fr[q]];
+                jb.dst_off = dst2[q];
+                jb.id = static_cast<uint32_t>(jobs.size());
+                jobs.push_back(jb);
+                items.push_back((len[fr[q]] + 11) / 12);
+            }
+            body_off[static_cast<uint64_t>(f) * peers + j++] = B.dst;
+            total += (dfs::kBodyStartPhase + dfs::kBodyFrameBytes + B.len_a + B.len_b + 15) & ~15ull;
+        }
+    }
+    body_off[static_cast<uint64_t>(nfiles) * peers] = total;
+    if (!bodies) return DFS_OK;  // layout query
+    if (!nfiles) return DFS_OK;
+    if ((end && !files) || !file_digest) return DFS_E_ARG;
+    hipStream_t s = c->stream();
+    const uint8_t* d_files = files;
+    const uint8_t* d_dig = file_digest;
+    char* d_out = bodies;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, files, end, s)) return rc;
+        d_files = c->buf[B_DATA_IN].as<uint8_t>();
+        if (int rc = put(c, B_DIG0, file_digest, 32ull * nfiles, s)) return rc;
+        d_dig = c->buf[B_DIG0].as<uint8_t>();
+        HIPC(c->buf[B_DATA_OUT].ensure(total));
+        d_out = c->buf[B_DATA_OUT].as<char>();
+    } else if (reinterpret_cast<uintptr_t>(bodies) & 15u) {
+        return DFS_E_ARG;
+    }
+    const uint32_t njobs = static_cast<uint32_t>(jobs.size());
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->b64_per) * dfs::kStreamBlock);
+    if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
+    if (int rc = put(c, B_DESC, desc.data(), desc.size() * sizeof(dfs::StoreBody), s)) return rc;
+    tm.begin(DFS_T_TOTAL, s);
+    HIPC(dfs::launch_store_body_frame(c->buf[B_DESC].as<dfs::StoreBody>(), static_cast<uint32_t>(desc.size()), d_dig,
+                                      d_out, s));
+    tm.begin(DFS_T_B64ENC, s);
+    HIPC(dfs::launch_b64_encode(d_files, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s, c->b64_per,
+                                c->b64_nt, c->b64_pair, 0u));
+    tm.end(DFS_T_B64ENC, s);
+    tm.end(DFS_T_TOTAL, s);
+    if (!dev) {
+        HIPC(hipMemcpyAsync(bodies, d_out, total, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    return DFS_OK;
+}
+
 }  // extern "C"

@@ -84,6 +84,23 @@ inline uint64_t enc_tiles(uint64_t len) {
     return (groups + kEncGroupsPerTile - 1) / kEncGroupsPerTile;
 }
 
+// One storeFragments request body (buildFragmentsJson, SN:629-642) carrying
+// fragments a and b (one digit each) of file `file`: framing bytes around
+// two Base64 payloads of len_a / len_b chars, at out + dst.
+struct StoreBody {
+    uint64_t dst;
+    uint64_t len_a;
+    uint64_t len_b;
+    uint32_t file;  // index into the fileId digests
+    uint16_t a, b;
+};
+constexpr uint32_t kBodyDataA = 111;     // first payload offset: {"fileId":"<64>","fragments":[{"index":"a","data":"
+constexpr uint32_t kBodyMidBytes = 24;   // "},{"index":"b","data":"
+constexpr uint32_t kBodyFrameBytes = 139;  // + the 4-byte "}]} suffix
+// Bodies start 1 byte past a 16-byte boundary so both payloads (at +111 and
+// +135 + len_a, len_a a multiple of 4) are dword aligned for the encoder.
+constexpr uint32_t kBodyStartPhase = 1;
+
 // Launchers (return hipError_t of the launch).
 // Persistent multi-message SHA-256.  `queue` is kShaQueueBytes of device
 // memory, zeroed by the launcher on `s` before the launch; the grid holds waves_per_simd waves
@@ -105,6 +122,9 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 // bit 1 = non-temporal loads.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
                              uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, int nt = 3);
+// Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
+hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
+                                   hipStream_t s);
 // Gather: job.src_off is an absolute device address of the fragment.
 hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
                          hipStream_t s);

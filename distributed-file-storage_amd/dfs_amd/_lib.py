@@ -78,6 +78,8 @@ SIGNATURES = {
     "dfs_synth_fill": (_int, [_vp, _vp, _vp, _u32, _u64, _u64]),
     "dfs_sha256_update_parts": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _u32]),
     "dfs_synth_fill_at": (_int, [_vp, _vp, _vp, _u32, _u64, _u64, _u64]),
+    "dfs_store_body_len": (_u64, [_u64, _u32, _u32, _u32]),
+    "dfs_store_bodies_build": (_int, [_vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _u32]),
 }
 
 _LIB = None

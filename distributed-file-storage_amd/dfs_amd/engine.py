@@ -249,6 +249,33 @@ class FragmentEngine:
             out.append(UploadResult(fd[f].tobytes().hex(), frags))
         return out
 
+    # -- sendFragmentsToPeers + buildFragmentsJson (SN:195-205, 629-642) ----------
+    def store_bodies(self, files: Sequence[bytes], nfrag: int, uploader: int,
+                     file_ids: Sequence[str]) -> List[List[Tuple[int, bytes]]]:
+        """storeFragments request bodies built on the device: per file, one
+        (peer node k, body) per peer k != uploader (0-based, ascending), each
+        carrying fragments k and k+1 mod nfrag (SN:199-200)."""
+        buf, spans = _pack(files)
+        nf = len(files)
+        peers = nfrag - 1
+        body_off = np.zeros(nf * peers + 1, dtype=np.uint64)
+        dig = np.frombuffer(b"".join(bytes.fromhex(h) for h in file_ids) or b"\0", dtype=np.uint8).copy()
+        check(lib().dfs_store_bodies_build(self._ctx, _ptr(buf), _ptr(spans), nf, nfrag, uploader, _ptr(dig), None,
+                                           _ptr(body_off), 0), "dfs_store_bodies_build (layout)")
+        out = np.zeros(max(int(body_off[-1]), 1), dtype=np.uint8)
+        check(lib().dfs_store_bodies_build(self._ctx, _ptr(buf), _ptr(spans), nf, nfrag, uploader, _ptr(dig),
+                                           _ptr(out), _ptr(body_off), 0), "dfs_store_bodies_build")
+        res = []
+        for f in range(nf):
+            peers_k = [k for k in range(nfrag) if k != uploader]
+            row = []
+            for j, k in enumerate(peers_k):
+                o = int(body_off[f * peers + j])
+                n = int(lib().dfs_store_body_len(len(files[f]), nfrag, k, (k + 1) % nfrag))
+                row.append((k, out[o:o + n].tobytes()))
+            res.append(row)
+        return res
+
     # -- handleDownload gather + verify (SN:419-458) ------------------------------
     def reassemble_verify(self, frags: Sequence[Sequence[Optional[bytes]]],
                           expected_file_ids: Optional[Sequence[str]] = None
@@ -372,6 +399,25 @@ def reassemble_device(engine: "FragmentEngine", frag_addr: np.ndarray, frag_len:
     if rc not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_CORRUPT):
         check(rc, "dfs_reassemble_verify")
     return status[:nfiles], dig[:nfiles]
+
+
+def store_bodies_layout(engine: "FragmentEngine", spans: np.ndarray, nfrag: int, uploader: int) -> np.ndarray:
+    """body_off of dfs_store_bodies_build for `spans` (layout query, no launch)."""
+    spans = np.ascontiguousarray(spans, dtype=np.uint64)
+    nf = len(spans)
+    body_off = np.zeros(nf * (nfrag - 1) + 1, dtype=np.uint64)
+    check(lib().dfs_store_bodies_build(engine.ctx, None, _ptr(spans), nf, nfrag, uploader, None, None,
+                                       _ptr(body_off), L.DFS_DEVICE_PTRS), "dfs_store_bodies_build (layout)")
+    return body_off
+
+
+def store_bodies_device(engine: "FragmentEngine", d_files: int, spans: np.ndarray, nfrag: int, uploader: int,
+                        d_file_digest: int, d_bodies: int, body_off: np.ndarray) -> None:
+    """dfs_store_bodies_build on device buffers (asynchronous on the engine's stream)."""
+    spans = np.ascontiguousarray(spans, dtype=np.uint64)
+    check(lib().dfs_store_bodies_build(engine.ctx, ctypes.c_void_p(d_files), _ptr(spans), len(spans), nfrag,
+                                       uploader, ctypes.c_void_p(d_file_digest), ctypes.c_void_p(d_bodies),
+                                       _ptr(body_off), L.DFS_DEVICE_PTRS), "dfs_store_bodies_build")
 
 
 class UploadPlan:

@@ -207,6 +207,34 @@ int dfs_download_batch(dfs_ctx* ctx, const char* b64, const dfs_span* b64_msgs, 
                        const uint8_t* expected_file_digest, uint8_t* out, const uint64_t* file_off,
                        int32_t* status, uint32_t flags);
 
+/* ---- storeFragments wire codec, sender side (SN:195-205, 629-642) ------- */
+/* Length of the storeFragments body carrying fragments a and b of a file of
+ * file_len bytes split into nfrag (buildFragmentsJson with two entries and
+ * one-digit indices): 139 framing bytes + both Base64 payloads. */
+uint64_t dfs_store_body_len(uint64_t file_len, uint32_t nfrag, uint32_t a, uint32_t b);
+
+/* sendFragmentsToPeers + buildFragmentsJson for a whole upload batch, built
+ * on the device: for every file f and every peer node k != uploader (0-based,
+ * ascending, SN:196-197) the request body
+ *   {"fileId":"<hex>","fragments":[{"index":"k","data":"<Base64 of fragment k>"},
+ *    {"index":"k+1 mod N","data":"<Base64 of fragment k+1 mod N>"}]}
+ * (SN:199-200, 629-642), byte-identical to the reference's, is written at
+ * bodies + body_off[f*(nfrag-1) + j], j = k's rank among the peers.  The
+ * Base64 is encoded straight from the file bytes into the body (no
+ * intermediate string, SN:636-637); the fileId hex comes from file_digest
+ * (raw 32 B per file, e.g. dfs_upload_batch's output).
+ *   body_off: nfiles*(nfrag-1)+1 entries, filled by the library (each
+ *             body starts 1 byte past a 16-byte boundary so both payloads
+ *             are dword aligned; last entry = bytes needed); a body's length
+ *             is dfs_store_body_len (the gap to the next start is unwritten)
+ *   bodies:   NULL = only fill body_off (layout query)
+ *   nfrag:    2..10 (one-digit indices keep both payloads dword aligned)
+ * With DFS_DEVICE_PTRS, files, file_digest and bodies are device memory
+ * (bodies 16-byte aligned) and the call is asynchronous. */
+int dfs_store_bodies_build(dfs_ctx* ctx, const uint8_t* files, const dfs_span* file_spans, uint32_t nfiles,
+                           uint32_t nfrag, uint32_t uploader, const uint8_t* file_digest, char* bodies,
+                           uint64_t* body_off, uint32_t flags);
+
 /* ---- prepared upload (descriptor build once, run many; device pointers) --- */
 /* flags: DFS_LAYOUT_FRAG_MAJOR stores the Base64 of fragment i of every file
  * contiguously ([fragment][file] order) so the bytes bound for one node are

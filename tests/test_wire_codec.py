@@ -1,0 +1,93 @@
+"""storeFragments wire codec, sender side: dfs_store_bodies_build vs the
+oracle's buildFragmentsJson restatement (SN:629-642) and the golden bodies of
+the reference's examples (uploaded at node 1).
+
+Bar: byte-identical request bodies.  The CPU test covers the length helper;
+the GPU tests build the bodies on the device through the C ABI."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+
+def _expected(data: bytes, nfrag: int, uploader: int):
+    fid = hashlib.sha256(data).hexdigest()
+    parts = [data[o:o + n] for o, n in O.py_split(len(data), nfrag)]
+    out = []
+    for k in range(nfrag):
+        if k == uploader:  # SN:197
+            continue
+        a, b = k, (k + 1) % nfrag  # SN:199-200
+        out.append((k, O.py_build_fragments_json(fid, [(a, parts[a]), (b, parts[b])]).encode()))
+    return out
+
+
+def test_store_body_len_matches_oracle():
+    from dfs_amd._lib import lib
+    rng = random.Random(5)
+    for _ in range(300):
+        n = rng.choice([0, 1, 2, 7, 28, 467, 2154, 9506, rng.randrange(0, 100000)])
+        nfrag = rng.randrange(2, 11)
+        k = rng.randrange(nfrag)
+        data = bytes(n)
+        parts = [data[o:o + m] for o, m in O.py_split(n, nfrag)]
+        b = (k + 1) % nfrag
+        want = len(O.py_build_fragments_json("0" * 64, [(k, parts[k]), (b, parts[b])]))
+        assert lib().dfs_store_body_len(n, nfrag, k, b) == want
+
+
+@pytest.mark.gpu
+def test_store_bodies_examples_golden(engine, golden, example_bytes):
+    for ex in golden["examples"]:
+        data = example_bytes[ex["name"]]
+        got = engine.store_bodies([data], 5, 0, [ex["fileId"]])[0]
+        assert [k for k, _ in got] == [1, 2, 3, 4]
+        for k, body in got:
+            assert body.decode() == ex["store_fragments_from_node1"][str(k + 1)]
+
+
+@pytest.mark.gpu
+def test_store_bodies_vs_oracle_random(engine):
+    rng = random.Random(11)
+    for nfrag in (2, 3, 5, 8, 10):
+        files = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 5, 11, 12, 13, 100, 777, 4099])))
+                 for _ in range(12)]
+        uploader = rng.randrange(nfrag)
+        ids = [hashlib.sha256(d).hexdigest() for d in files]
+        got = engine.store_bodies(files, nfrag, uploader, ids)
+        for d, row in zip(files, got):
+            assert row == _expected(d, nfrag, uploader)
+
+
+@pytest.mark.gpu
+def test_store_bodies_device_buffers(engine):
+    """Device pointers (the bench path): 96 synthetic files of mixed sizes,
+    fileIds from the device upload, bodies checked against the oracle."""
+    import torch
+    import dfs_amd
+    from dfs_amd.engine import store_bodies_layout, store_bodies_device
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(0, 300_000, 96).astype(np.uint64)
+    sizes[:4] = [0, 1, 1 << 20, 209_716 * 5 + 3]
+    offs = np.concatenate([[0], np.cumsum((sizes + 63) // 64 * 64)[:-1]]).astype(np.uint64)
+    spans = np.stack([offs, sizes], axis=1)
+    nf, nfrag, up = len(sizes), 5, 2
+    dev = torch.device("cuda", 0)
+    files = torch.empty(int(offs[-1] + sizes[-1]) + 64, dtype=torch.uint8, device=dev)
+    dfs_amd.synth_fill(engine, files.data_ptr(), spans, 0, 0x5EED5EED)
+    digests = torch.frombuffer(bytearray(b"".join(hashlib.sha256(O.c_synth(f, 0, int(sizes[f]))).digest()
+                                                  for f in range(nf))), dtype=torch.uint8).to(dev)
+    body_off = store_bodies_layout(engine, spans, nfrag, up)
+    bodies = torch.zeros(int(body_off[-1]), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    store_bodies_device(engine, files.data_ptr(), spans, nfrag, up, digests.data_ptr(), bodies.data_ptr(), body_off)
+    torch.cuda.synchronize(dev)
+    host = bodies.cpu().numpy()
+    for f in range(nf):
+        want = _expected(O.c_synth(f, 0, int(sizes[f])), nfrag, up)
+        for j, (k, body) in enumerate(want):
+            o = int(body_off[f * (nfrag - 1) + j])
+            assert host[o:o + len(body)].tobytes() == body, (f, k)
