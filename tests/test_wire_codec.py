@@ -46,7 +46,8 @@ def test_store_bodies_examples_golden(engine, golden, example_bytes):
         got = engine.store_bodies([data], 5, 0, [ex["fileId"]])[0]
         assert [k for k, _ in got] == [1, 2, 3, 4]
         for k, body in got:
-            assert body.decode() == ex["store_fragments_from_node1"][str(k + 1)]
+            want = ex["store_fragments_from_node1"][str(k + 1)]  # the body, or its SHA-256 for large files
+            assert (body.decode() if want.startswith("{") else hashlib.sha256(body).hexdigest()) == want
 
 
 @pytest.mark.gpu
