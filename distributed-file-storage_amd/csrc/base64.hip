@@ -484,3 +484,110 @@ hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const ui
 }
 
 }  // namespace dfs
+
+// ---------------------------------------------------------------------------
+// storeFragments body parse (receiver, handleInternalStoreFragments
+// SN:265-279 / parseJson SN:704-753) for bodies in buildFragmentsJson's exact
+// form: two entries with one-digit indices.  One wave per body checks the
+// framing bytes and finds each payload's closing quote with a wave-wide scan
+// (16 bytes per lane per step, dword compares, first hit by ballot).  A body
+// in any other form gets status 1 and is left to the host's parseJson.
+// ---------------------------------------------------------------------------
+namespace dfs {
+namespace {
+
+// First '"' at or after body position `from` (< L), or L if none.  Loads are
+// 16-byte aligned blocks that start inside [body, body + L), so they never
+// cross a page the body does not touch.
+__device__ uint64_t scan_quote(const char* __restrict__ body, uint64_t from, uint64_t L) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uintptr_t b = reinterpret_cast<uintptr_t>(body);
+    uintptr_t blk = (b + from) & ~static_cast<uintptr_t>(15);
+    for (; blk < b + L; blk += 1024) {
+        const uintptr_t my = blk + 16u * lane;
+        uint32_t hit = 16;  // byte index of the first quote in my block
+        if (my < b + L) {
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(my));
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 3; q >= 0; --q) {
+                uint32_t y = w[q] ^ 0x22222222u;
+                // bytes before `from` never match
+                const intptr_t lo = static_cast<intptr_t>(b + from) - static_cast<intptr_t>(my + 4 * q);
+                if (lo >= 4) y = 0xffffffffu;
+                else if (lo > 0) y |= (1u << (8 * lo)) - 1u;
+                const uint32_t z = (y - 0x01010101u) & ~y & 0x80808080u;
+                if (z) hit = 4 * q + (__builtin_ctz(z) >> 3);
+            }
+        }
+        const uint64_t m = __ballot(hit < 16);
+        if (m) {
+            const uint32_t first = __builtin_ctzll(m);
+            const uint32_t h = __shfl(hit, first, 64);
+            const uint64_t pos = (blk + 16u * first + h) - b;
+            return pos < L ? pos : L;
+        }
+    }
+    return L;
+}
+
+// Wave-parallel compare of n framing bytes at body + at with text (digit
+// placeholders '0' at index dpos match any decimal digit).
+__device__ bool frame_ok(const char* __restrict__ body, uint64_t at, const char* text, uint32_t n, uint32_t dpos) {
+    const uint32_t lane = threadIdx.x & 63u;
+    bool ok = true;
+    for (uint32_t i = lane; i < n; i += 64) {
+        const char c = body[at + i];
+        ok &= (i == dpos) ? (c >= '0' && c <= '9') : (c == text[i]);
+    }
+    return __ballot(!ok) == 0;
+}
+
+__global__ __launch_bounds__(256) void store_body_parse_kernel(const char* __restrict__ in,
+                                                               const uint64_t* __restrict__ spans, uint32_t n,
+                                                               BodyParse* __restrict__ out,
+                                                               char* __restrict__ file_ids) {
+    const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (k >= n) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const char* body = in + spans[2 * k];
+    const uint64_t L = spans[2 * k + 1];
+    BodyParse r{};
+    r.status = 1;
+    bool ok = L >= kBodyFrameBytes;
+    // {"fileId":"<64 chars>","fragments":[{"index":"d","data":"
+    if (ok) ok = frame_ok(body, 0, kBodyPrefix, 11, ~0u) &&
+                 frame_ok(body, 75, kBodyPrefix + 75, kBodyDataA - 75, kBodyDataA - 11 - 75);
+    if (ok) ok = __ballot(body[11 + lane] == '"') == 0;  // the fileId holds no quote
+    if (ok) {
+        const uint64_t qa = scan_quote(body, kBodyDataA, L);
+        ok = qa + kBodyMidBytes + 4 <= L && frame_ok(body, qa, kBodyMid, kBodyMidBytes, kBodyMidBytes - 11);
+        if (ok) {
+            const uint64_t sb = qa + kBodyMidBytes;
+            const uint64_t qb = scan_quote(body, sb, L);
+            ok = qb + 4 == L && frame_ok(body, qb, kBodySuffix, 4, ~0u);
+            if (ok) {
+                r.off_a = kBodyDataA;
+                r.len_a = qa - kBodyDataA;
+                r.off_b = sb;
+                r.len_b = qb - sb;
+                r.a = static_cast<uint16_t>(body[kBodyDataA - 11] - '0');
+                r.b = static_cast<uint16_t>(body[qa + kBodyMidBytes - 11] - '0');
+                r.status = 0;
+            }
+        }
+    }
+    if (r.status == 0) file_ids[64ull * k + lane] = body[11 + lane];
+    if (lane == 0) out[k] = r;
+}
+
+}  // namespace
+
+hipError_t launch_store_body_parse(const char* in, const uint64_t* spans, uint32_t n, BodyParse* out,
+                                   char* file_ids, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(store_body_parse_kernel, dim3((n + 3) / 4), dim3(256), 0, s, in, spans, n, out, file_ids);
+    return hipGetLastError();
+}
+
+}  // namespace dfs

@@ -209,6 +209,7 @@ const char* dfs_strerror(int code) {
         case DFS_E_CORRUPT: return "File corrupted";
         case DFS_E_FRAG_MISMATCH: return "Hash mismatch on fragment";
         case DFS_E_NODEV: return "no gfx950 (MI355X) device available";
+        case DFS_E_WIRE: return "storeFragments body not in buildFragmentsJson form (parse it with parseJson)";
         default: return "unknown error";
     }
 }
@@ -1168,6 +1169,84 @@ int dfs_store_bodies_build(dfs_ctx* c, const uint8_t* files, const dfs_span* fil
     if (!dev) {
         HIPC(hipMemcpyAsync(bodies, d_out, total, hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
+    }
+    return DFS_OK;
+}
+
+// storeFragments wire codec, receiver side: handleInternalStoreFragments
+// (SN:265-293) for bodies in buildFragmentsJson form.
+int dfs_store_bodies_receive(dfs_ctx* c, const char* bodies, const dfs_span* body_spans, uint32_t n, uint8_t* out,
+                             uint64_t* out_off, uint32_t* frag_index, uint64_t* frag_off, uint64_t* frag_len,
+                             uint8_t* digests, char* file_ids, int32_t* status, uint32_t flags) {
+    if (!c || !out_off ||
+        (n && (!body_spans || !frag_index || !frag_off || !frag_len || !digests || !file_ids || !status)))
+        return DFS_E_ARG;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    uint64_t end = 0, total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        out_off[i] = total;
+        total += 3 * ((body_spans[i].len + 3) / 4);  // >= both decoded payloads
+        end = std::max(end, body_spans[i].off + body_spans[i].len);
+    }
+    out_off[n] = total;
+    if (!n) return DFS_OK;
+    if ((end && !bodies) || (total && !out)) return DFS_E_ARG;
+    std::vector<dfs::BodyParse> parsed(n);
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (int rc = enter(c)) return rc;
+        hipStream_t s = c->stream();
+        const char* d_in = bodies;
+        if (!dev) {
+            if (int rc = put(c, B_DATA_IN, bodies, end, s)) return rc;
+            d_in = c->buf[B_DATA_IN].as<char>();
+        }
+        if (int rc = put(c, B_JOBS, body_spans, sizeof(dfs_span) * n, s)) return rc;
+        HIPC(c->buf[B_DESC].ensure(sizeof(dfs::BodyParse) * n));
+        HIPC(c->buf[B_DIG1].ensure(64ull * n));
+        HIPC(dfs::launch_store_body_parse(d_in, c->buf[B_JOBS].as<uint64_t>(), n, c->buf[B_DESC].as<dfs::BodyParse>(),
+                                          c->buf[B_DIG1].as<char>(), s));
+        HIPC(hipMemcpyAsync(parsed.data(), c->buf[B_DESC].p, sizeof(dfs::BodyParse) * n, hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(file_ids, c->buf[B_DIG1].p, 64ull * n, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    // Decode each payload into the body's output slot and hash it (SN:280-282).
+    std::vector<dfs_span> msgs;
+    std::vector<uint64_t> dst, len;
+    std::vector<int32_t> st;
+    std::vector<uint32_t> who;
+    for (uint32_t i = 0; i < n; ++i) {
+        status[i] = parsed[i].status ? DFS_E_WIRE : DFS_OK;
+        frag_len[2 * i] = frag_len[2 * i + 1] = 0;
+        frag_off[2 * i] = frag_off[2 * i + 1] = out_off[i];
+        if (parsed[i].status) {
+            frag_index[2 * i] = frag_index[2 * i + 1] = UINT32_MAX;
+            continue;
+        }
+        const dfs::BodyParse& p = parsed[i];
+        frag_index[2 * i] = p.a;
+        frag_index[2 * i + 1] = p.b;
+        msgs.push_back(dfs_span{body_spans[i].off + p.off_a, p.len_a});
+        dst.push_back(out_off[i]);
+        msgs.push_back(dfs_span{body_spans[i].off + p.off_b, p.len_b});
+        dst.push_back(out_off[i] + dfs_b64_decoded_cap(p.len_a));
+        frag_off[2 * i + 1] = dst.back();
+        who.push_back(i);
+    }
+    if (msgs.empty()) return DFS_OK;
+    len.resize(msgs.size());
+    st.resize(msgs.size());
+    std::vector<uint8_t> dig(32 * msgs.size());
+    int rc = dfs_receive_fragments_batch(c, bodies, msgs.data(), static_cast<uint32_t>(msgs.size()), out, dst.data(),
+                                         len.data(), dig.data(), st.data(), flags);
+    if (rc != DFS_OK && rc != DFS_E_DECODE) return rc;
+    for (size_t k = 0; k < who.size(); ++k) {
+        const uint32_t i = who[k];
+        for (int q = 0; q < 2; ++q) {
+            frag_len[2 * i + q] = len[2 * k + q];
+            std::memcpy(digests + 64ull * i + 32 * q, dig.data() + 64 * k + 32 * q, 32);
+            if (st[2 * k + q] != DFS_OK) status[i] = DFS_E_DECODE;  // SN:281 IllegalArgumentException
+        }
     }
     return DFS_OK;
 }

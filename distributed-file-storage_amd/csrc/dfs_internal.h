@@ -101,6 +101,14 @@ constexpr uint32_t kBodyFrameBytes = 139;  // + the 4-byte "}]} suffix
 // +135 + len_a, len_a a multiple of 4) are dword aligned for the encoder.
 constexpr uint32_t kBodyStartPhase = 1;
 
+// Receiver-side parse of one storeFragments body (offsets relative to the
+// body; status 0 = buildFragmentsJson form, 1 = any other form).
+struct BodyParse {
+    uint64_t off_a, len_a, off_b, len_b;
+    int32_t status;
+    uint16_t a, b;
+};
+
 // Launchers (return hipError_t of the launch).
 // Persistent multi-message SHA-256.  `queue` is kShaQueueBytes of device
 // memory, zeroed by the launcher on `s` before the launch; the grid holds waves_per_simd waves
@@ -125,6 +133,10 @@ hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njo
 // Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
 hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
                                    hipStream_t s);
+// Parse n bodies (spans = n x {off, len} into `in`, device memory); the
+// 64 fileId chars of body k go to file_ids + 64k.
+hipError_t launch_store_body_parse(const char* in, const uint64_t* spans, uint32_t n, BodyParse* out,
+                                   char* file_ids, hipStream_t s);
 // Gather: job.src_off is an absolute device address of the fragment.
 hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
                          hipStream_t s);

@@ -25,6 +25,7 @@ DFS_E_MISSING = -5
 DFS_E_CORRUPT = -6
 DFS_E_FRAG_MISMATCH = -7
 DFS_E_NODEV = -8
+DFS_E_WIRE = -9
 
 DFS_DEVICE_PTRS = 0x1
 DFS_NO_FILEID = 0x2
@@ -80,6 +81,7 @@ SIGNATURES = {
     "dfs_synth_fill_at": (_int, [_vp, _vp, _vp, _u32, _u64, _u64, _u64]),
     "dfs_store_body_len": (_u64, [_u64, _u32, _u32, _u32]),
     "dfs_store_bodies_build": (_int, [_vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _u32]),
+    "dfs_store_bodies_receive": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
 }
 
 _LIB = None

@@ -276,6 +276,37 @@ class FragmentEngine:
             res.append(row)
         return res
 
+    def store_receive(self, bodies: Sequence[bytes]):
+        """handleInternalStoreFragments (SN:265-293) on the device for bodies in
+        buildFragmentsJson form.  Per body: (status, fileId or None,
+        [(index, bytes, sha256 hex)] for both entries or [])."""
+        n = len(bodies)
+        buf, spans = _pack(bodies)
+        out_off = np.zeros(n + 1, dtype=np.uint64)
+        cap = sum(3 * ((len(b) + 3) // 4) for b in bodies)
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        idx = np.zeros(max(2 * n, 1), dtype=np.uint32)
+        foff = np.zeros(max(2 * n, 1), dtype=np.uint64)
+        flen = np.zeros(max(2 * n, 1), dtype=np.uint64)
+        dig = np.zeros((max(n, 1), 2, 32), dtype=np.uint8)
+        ids = np.zeros((max(n, 1), 64), dtype=np.uint8)
+        status = np.zeros(max(n, 1), dtype=np.int32)
+        check(lib().dfs_store_bodies_receive(self._ctx, _ptr(buf), _ptr(spans), n, _ptr(out), _ptr(out_off),
+                                             _ptr(idx), _ptr(foff), _ptr(flen), _ptr(dig), _ptr(ids), _ptr(status), 0),
+              "dfs_store_bodies_receive")
+        res = []
+        for i in range(n):
+            st = int(status[i])
+            if st == L.DFS_E_WIRE:
+                res.append((st, None, []))
+                continue
+            frags = []
+            for q in range(2):
+                o, ln = int(foff[2 * i + q]), int(flen[2 * i + q])
+                frags.append((int(idx[2 * i + q]), out[o:o + ln].tobytes(), dig[i, q].tobytes().hex()))
+            res.append((st, ids[i].tobytes().decode("latin-1"), frags))
+        return res
+
     # -- handleDownload gather + verify (SN:419-458) ------------------------------
     def reassemble_verify(self, frags: Sequence[Sequence[Optional[bytes]]],
                           expected_file_ids: Optional[Sequence[str]] = None

@@ -45,6 +45,8 @@ extern "C" {
 #define DFS_E_CORRUPT (-6)      /* "File corrupted": SHA-256(file)!=fileId (SN:455)*/
 #define DFS_E_FRAG_MISMATCH (-7) /* "Hash mismatch on fragment" (SN:250-257)      */
 #define DFS_E_NODEV (-8)        /* no gfx950 device                               */
+#define DFS_E_WIRE (-9)         /* storeFragments body not in buildFragmentsJson  */
+                                /* form: the host parses it with parseJson        */
 
 /* Flags. */
 #define DFS_DEVICE_PTRS 0x1u    /* data pointers are device pointers; async       */
@@ -234,6 +236,30 @@ uint64_t dfs_store_body_len(uint64_t file_len, uint32_t nfrag, uint32_t a, uint3
 int dfs_store_bodies_build(dfs_ctx* ctx, const uint8_t* files, const dfs_span* file_spans, uint32_t nfiles,
                            uint32_t nfrag, uint32_t uploader, const uint8_t* file_digest, char* bodies,
                            uint64_t* body_off, uint32_t flags);
+
+/* Receiver side, handleInternalStoreFragments (SN:265-293) for a batch of
+ * storeFragments request bodies in buildFragmentsJson form (what
+ * dfs_store_bodies_build and the reference's senders write: two entries,
+ * one-digit indices): the device parses every body (SN:268-272, parseJson
+ * SN:704-753), Base64-decodes both payloads (SN:281) and SHA-256s the
+ * decoded fragments (SN:282).  Per body i:
+ *   file_ids[64i..]      the fileId string (64 chars, not NUL-terminated)
+ *   frag_index[2i+q]     entry q's "index" (q = 0, 1), in body order
+ *   out_off              n+1 entries filled by the library: body i's slot
+ *                        in out (3*ceil(len/4) bytes; out_off[n] = bytes
+ *                        needed)
+ *   out + frag_off[2i+q] entry q's decoded bytes (frag_len[2i+q] of them);
+ *                        digests[64i + 32q] their SHA-256,
+ *                        the hashes of the reply (buildHashResponse, SN:644-655)
+ *   status[i]            0, DFS_E_DECODE (IllegalArgumentException, SN:281:
+ *                        no reply) or DFS_E_WIRE (body in another form:
+ *                        parse it on the host with the reference's parseJson
+ *                        and use dfs_receive_fragments_batch)
+ * bodies/out device memory with DFS_DEVICE_PTRS; synchronous. */
+int dfs_store_bodies_receive(dfs_ctx* ctx, const char* bodies, const dfs_span* body_spans, uint32_t n,
+                             uint8_t* out, uint64_t* out_off, uint32_t* frag_index, uint64_t* frag_off,
+                             uint64_t* frag_len, uint8_t* digests, char* file_ids, int32_t* status,
+                             uint32_t flags);
 
 /* ---- prepared upload (descriptor build once, run many; device pointers) --- */
 /* flags: DFS_LAYOUT_FRAG_MAJOR stores the Base64 of fragment i of every file

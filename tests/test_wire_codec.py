@@ -92,3 +92,48 @@ def test_store_bodies_device_buffers(engine):
         for j, (k, body) in enumerate(want):
             o = int(body_off[f * (nfrag - 1) + j])
             assert host[o:o + len(body)].tobytes() == body, (f, k)
+
+
+def _oracle_receive(body: bytes):
+    st, fid, done, _resp = O.py_store_fragments(body)
+    return st, fid, done
+
+
+@pytest.mark.gpu
+def test_store_receive_roundtrip_vs_oracle(engine):
+    """Bodies from the device builder, received on the device: parse, decode,
+    hash == the oracle's handleInternalStoreFragments restatement."""
+    rng = random.Random(21)
+    files = [bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 2, 3, 4, 5, 47, 48, 49, 1000, 70001])))
+             for _ in range(10)]
+    ids = [hashlib.sha256(d).hexdigest() for d in files]
+    for nfrag in (2, 5, 10):
+        built = engine.store_bodies(files, nfrag, nfrag - 1, ids)
+        bodies = [b for row in built for _, b in row]
+        got = engine.store_receive(bodies)
+        for body, (st, fid, frags) in zip(bodies, got):
+            ost, ofid, done = _oracle_receive(body)
+            assert ost is None and st == 0
+            assert fid == ofid
+            assert [(i, d, h) for i, d, h in frags] == done
+
+
+@pytest.mark.gpu
+def test_store_receive_examples_and_bad_bodies(engine, golden, example_bytes):
+    from dfs_amd._lib import DFS_E_DECODE, DFS_E_WIRE
+    teste = golden["examples"][0]
+    good = teste["store_fragments_from_node1"]["5"].encode()  # {4, 0}
+    bad_b64 = good.replace(b"VGVzdGUg", b"VGVzd*Ug")      # entry 2 not Base64 -> IAE after entry 1
+    bad_pad = good.replace(b"dWl2by4=", b"dWl2b")          # 5 chars: dangling char -> IAE on entry 1
+    spaced = good.replace(b'","data"', b'", "data"', 1)  # parseJson accepts it, the device form does not
+    three = good.replace(b"]}", b',{"index":"1","data":"Zm9v"}]}')
+    got = engine.store_receive([good, bad_b64, bad_pad, spaced, three, b"", b"{}"])
+    st, fid, frags = got[0]
+    assert st == 0 and fid == teste["fileId"]
+    assert [(i, h) for i, _, h in frags] == [(4, teste["fragments"][4]["sha256"]), (0, teste["fragments"][0]["sha256"])]
+    assert got[1][0] == DFS_E_DECODE and _oracle_receive(bad_b64)[0] == "IllegalArgumentException"
+    assert got[1][2][0][2] == teste["fragments"][4]["sha256"]  # entry 1 was processed, as SN:280-285 does
+    assert got[2][0] == DFS_E_DECODE and _oracle_receive(bad_pad)[0] == "IllegalArgumentException"
+    for k in (3, 4, 5, 6):
+        assert got[k][0] == DFS_E_WIRE
+    assert _oracle_receive(spaced)[0] is None  # the host parser's case
