@@ -266,7 +266,7 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
             "note": "wall_ms includes host-side job planning per call; gbps = file bytes / device time"}
 
 
-def wire_leg(args, eng, files, fd, S, N, F, dev, log):
+def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
     """storeFragments request bodies on the device (SN:195-205 + 629-642):
     node 1 (0-based 0) uploads; for each sampled file the N-1 peer bodies
     {"fileId":..,"fragments":[{k},{k+1}]} with the Base64 encoded straight
@@ -308,8 +308,34 @@ def wire_leg(args, eng, files, fd, S, N, F, dev, log):
                 want = O.py_build_fragments_json(fid, [(k, parts[k]), (((k + 1) % N), parts[(k + 1) % N])]).encode()
                 o = int(body_off[f * (N - 1) + j])
                 ok &= bodies[o:o + len(want)].cpu().numpy().tobytes() == want
+    # Receiver side (handleInternalStoreFragments, SN:265-293) over the same
+    # bodies: device parse, decode of both entries, SHA-256 of each; the
+    # digests must equal the upload-time fragment digests (the sender's check,
+    # SN:248-257).  Synchronous call, wall-clock timed.
+    from dfs_amd.engine import store_receive_device, store_receive_out_bytes
     lens = split(S, N)
-    body_bytes = sum(139 + 4 * ((lens[k] + 2) // 3) + 4 * ((lens[(k + 1) % N] + 2) // 3) for k in range(1, N))
+    blen = np.array([139 + 4 * ((lens[k] + 2) // 3) + 4 * ((lens[(k + 1) % N] + 2) // 3) for k in range(1, N)],
+                    dtype=np.uint64)
+    bspans = np.stack([body_off[:-1], np.tile(blen, R)], axis=1)
+    rout = torch.empty(store_receive_out_bytes(bspans) + 16, dtype=torch.uint8, device=dev)
+    store_receive_device(eng, bodies.data_ptr(), bspans, rout.data_ptr())
+    torch.cuda.synchronize(dev)
+    rw = []
+    for _ in range(max(1, args.dl_steps)):
+        t0 = time.perf_counter()
+        st, idx, foff, flen, rdig, ids = store_receive_device(eng, bodies.data_ptr(), bspans, rout.data_ptr())
+        rw.append(time.perf_counter() - t0)
+    frdh = frd[:R * N * 32].view(R, N, 32).cpu().numpy()
+    want_idx = np.tile(np.array([[k, (k + 1) % N] for k in range(1, N)], dtype=np.uint32), (R, 1))
+    rok = bool((st == 0).all()) and bool((idx == want_idx).all())
+    fi = np.repeat(np.arange(R), N - 1)
+    rok = rok and bool((rdig == frdh[fi[:, None], want_idx]).all())
+    fdh = fd[:R * 32].view(R, 32).cpu().numpy()
+    hexes = np.frombuffer(b"".join(fdh[f].tobytes().hex().encode() for f in range(R)), dtype=np.uint8).reshape(R, 64)
+    rok = rok and bool((ids == hexes[fi]).all())
+    del rout
+    recv_ms = float(np.mean(rw)) * 1e3
+    body_bytes = int(blen.sum())
     raw_read = sum(lens[k] + lens[(k + 1) % N] for k in range(1, N))
     moved = R * (body_bytes + raw_read)
     ms = float(np.mean(tot))
@@ -319,8 +345,12 @@ def wire_leg(args, eng, files, fd, S, N, F, dev, log):
             "encode_ms": round(float(np.mean(enc)), 3), "body_gbs": round(R * body_bytes / (ms / 1e3) / 1e9, 1),
             "hbm_gbs": round(moved / (ms / 1e3) / 1e9, 1), "hbm_frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "ok": bool(ok),
+            "receive_wall_ms": round(recv_ms, 3), "receive_body_gbs": round(R * body_bytes / (recv_ms / 1e3) / 1e9, 1),
+            "receive_ok": rok,
             "note": "bodies byte-identical to buildFragmentsJson (SN:629-642); hbm_gbs = raw fragment bytes read "
-                    "+ body bytes written per second"}
+                    "+ body bytes written per second; receive = device parse + decode + SHA-256 of every entry "
+                    "(synchronous call, wall clock incl. host job planning), digests == upload-time fragment "
+                    "digests"}
 
 
 def long_leg(args):
@@ -547,7 +577,7 @@ def main():
             result["download"] = {"error": repr(e)[:300]}
     if not args.no_wire:
         try:
-            result["wire"] = wire_leg(args, eng, files, fd, S, N, F, dev, log)
+            result["wire"] = wire_leg(args, eng, files, fd, frd, S, N, F, dev, log)
         except Exception as e:
             result["wire"] = {"error": repr(e)[:300]}
     if world > 1 and not args.no_replicate:

@@ -451,6 +451,30 @@ def store_bodies_device(engine: "FragmentEngine", d_files: int, spans: np.ndarra
                                        _ptr(body_off), L.DFS_DEVICE_PTRS), "dfs_store_bodies_build")
 
 
+def store_receive_device(engine: "FragmentEngine", d_bodies: int, spans: np.ndarray, d_out: int):
+    """dfs_store_bodies_receive on device buffers.  Returns (status,
+    frag_index (n, 2), frag_off (n, 2), frag_len (n, 2), digests (n, 2, 32),
+    file_ids (n, 64) uint8).  d_out must hold store_receive_out_bytes(spans)."""
+    spans = np.ascontiguousarray(spans, dtype=np.uint64)
+    n = len(spans)
+    out_off = np.zeros(n + 1, dtype=np.uint64)
+    idx = np.zeros((max(n, 1), 2), dtype=np.uint32)
+    foff = np.zeros((max(n, 1), 2), dtype=np.uint64)
+    flen = np.zeros((max(n, 1), 2), dtype=np.uint64)
+    dig = np.zeros((max(n, 1), 2, 32), dtype=np.uint8)
+    ids = np.zeros((max(n, 1), 64), dtype=np.uint8)
+    status = np.zeros(max(n, 1), dtype=np.int32)
+    check(lib().dfs_store_bodies_receive(engine.ctx, ctypes.c_void_p(d_bodies), _ptr(spans), n,
+                                         ctypes.c_void_p(d_out), _ptr(out_off), _ptr(idx), _ptr(foff), _ptr(flen),
+                                         _ptr(dig), _ptr(ids), _ptr(status), L.DFS_DEVICE_PTRS),
+          "dfs_store_bodies_receive")
+    return status[:n], idx[:n], foff[:n], flen[:n], dig[:n], ids[:n]
+
+
+def store_receive_out_bytes(spans: np.ndarray) -> int:
+    return int(sum(3 * ((int(ln) + 3) // 4) for ln in np.asarray(spans)[:, 1]))
+
+
 class UploadPlan:
     """dfs_upload_plan over device-resident (torch) buffers — the bench path."""
 
