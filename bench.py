@@ -162,11 +162,22 @@ def replication_leg(args, eng, files, S, N, dev, log):
     dist.all_reduce(sent_t)
     ok_ex = all(len(held[f][0]) == sum(table[r][f] for r in range(world)) for f in P.gpu_fragments(me, N, world))
 
+    # The reference's star fan-out (SN:195-205) as one all-to-all: every link busy at once.
+    (held_s, _t), t_star = timed(lambda: P.exchange_upload_star(b64, group_off, N), args.rep_steps)
+    ok_ex = ok_ex and all(torch.equal(held_s[f][0], held[f][0]) for f in P.gpu_fragments(me, N, world))
+    need = [P.gpu_fragments(g, N, world) for g in range(world)]
+    sent_s = sum(table[me][f] for g in range(world) if g != me for f in need[g])
+    sent_st = torch.tensor([sent_s], dtype=torch.float64, device=dev)
+    dist.all_reduce(sent_st)
+    del held_s
+
     offline = {world - 1}
     fetched, t_fetch = timed(lambda: P.exchange_download(held, table, N, offline=offline, device=dev), args.rep_steps)
     result = {"files_per_gpu": R, "nodes": N, "node_to_gpu": "node k on GPU k mod W",
               "upload_exchange_ms": round(t_up * 1e3, 3),
               "upload_exchange_gbps_per_gpu": round(sent_t.item() / world / t_up / 1e9, 2),
+              "star_exchange_ms": round(t_star * 1e3, 3),
+              "star_exchange_gbps_per_gpu": round(sent_st.item() / world / t_star / 1e9, 2),
               "exchange_sizes_ok": bool(ok_ex), "offline_gpu": world - 1,
               "degraded_fetch_ms": round(t_fetch * 1e3, 3)}
     status_ok = True

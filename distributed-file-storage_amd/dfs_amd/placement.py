@@ -21,6 +21,9 @@ The exchange realises the reference's pair set in two steps:
      node k <-> GPU k+1), one xGMI link per GPU.
 After both steps every GPU holds exactly the fragments of the nodes it hosts.
 
+`exchange_upload_star` realises the reference's star fan-out itself as one
+all-to-all (every link busy at once); it yields the same holdings.
+
 `download_sources` mirrors SN:427-440's candidate order for a degraded fetch
 (one GPU offline) and `exchange_download` moves each requester's fragments back
 from the holders for decode + verify + reassembly (dfs_download_batch).
@@ -155,6 +158,40 @@ def exchange_upload(b64: torch.Tensor, group_off: Sequence[int], nfrag: int
                 ops.append(dist.P2POp(dist.irecv, buf, src))
             held[f] = (buf, per_src[f])
     _p2p(ops)
+    return held, table
+
+
+def exchange_upload_star(b64: torch.Tensor, group_off: Sequence[int], nfrag: int
+                         ) -> Tuple[Dict[int, Tuple[torch.Tensor, List[int]]], List[List[int]]]:
+    """The reference's own fan-out (SN:195-205: the uploader sends every peer
+    its pair directly) as ONE all-to-all: rank r sends GPU g the groups of
+    every fragment g must hold (gpu_fragments), so each fragment group leaves
+    its source once per holder and every xGMI link carries traffic at once
+    (SURVEY §8f rank 3), instead of the ring's scatter + forward over one
+    link.  Same result format as exchange_upload."""
+    world, me, dev = dist.get_world_size(), dist.get_rank(), b64.device
+    sizes = [int(group_off[f + 1] - group_off[f]) for f in range(nfrag)]
+    table = _all_sizes(sizes, dev).cpu().tolist()  # table[rank][f]
+    need = [gpu_fragments(g, nfrag, world) for g in range(world)]
+    parts, in_split = [], []
+    for g in range(world):
+        in_split.append(sum(sizes[f] for f in need[g]))
+        parts += [b64[int(group_off[f]):int(group_off[f + 1])] for f in need[g]]
+    send = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=dev)
+    out_split = [sum(table[r][f] for f in need[me]) for r in range(world)]
+    flat = torch.empty(sum(out_split), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(flat, send, out_split, in_split)
+    starts = [sum(out_split[:r]) for r in range(world)]
+    recv = [flat[starts[r]:starts[r] + out_split[r]] for r in range(world)]
+    held: Dict[int, Tuple[torch.Tensor, List[int]]] = {}
+    pos = [0] * world
+    for f in need[me]:
+        per = [table[r][f] for r in range(world)]
+        pieces = []
+        for r in range(world):
+            pieces.append(recv[r][pos[r]:pos[r] + per[r]])
+            pos[r] += per[r]
+        held[f] = (torch.cat(pieces), per)
     return held, table
 
 

@@ -67,6 +67,11 @@ def _worker(rank, world, port, nfrag, nfiles, offline, q):
             got = held[f][0].numpy().tobytes()
             assert got == exp, (rank, f)
             assert held[f][1] == [table[r][f] for r in range(world)]
+        # the star fan-out as one all-to-all yields the same holdings
+        star, table2 = P.exchange_upload_star(t, off, nfrag)
+        assert table2 == table and sorted(star) == want
+        for f in want:
+            assert torch.equal(star[f][0], held[f][0]) and star[f][1] == held[f][1], (rank, f)
         # degraded read: my own fragments back from the holders
         got = P.exchange_download(held, table, nfrag, offline=offline)
         if rank not in offline:
