@@ -406,8 +406,11 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
         if (item == 0xffffffffu) break;
         if (item < n_long) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
-        uint64_t t_start = 0;
-        if (census) t_start = __builtin_amdgcn_s_memrealtime();
+        uint64_t t_start = 0, c_start = 0;
+        if (census) {
+            t_start = __builtin_amdgcn_s_memrealtime();
+            c_start = __builtin_amdgcn_s_memtime();
+        }
         const uint32_t gid = item * 64u + lane;
         // ENC: uniform trip count (the wave's longest message, in an SGPR).
         // A divergent loop exit inside the three-phase body made hipcc copy
@@ -552,9 +555,10 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
         }
         if (census && lane == 0u) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;  // shader clocks of this item
             uint32_t* c = census + 4ull * item;
             c[0] = hw_id();
-            c[1] = xcc_id();
+            c[1] = (xcc_id() << 28) | static_cast<uint32_t>(cyc > 0x0fffffffu ? 0x0fffffffu : cyc);
             c[2] = static_cast<uint32_t>(t_start);
             c[3] = static_cast<uint32_t>(t_end);
         }

@@ -10,7 +10,7 @@ a = np.fromfile(sys.argv[1], dtype=np.uint32).reshape(-1, 4).astype(np.int64)
 n_long = int(sys.argv[2])
 t0 = (a[:, 2] - a[:, 2].min()) / 1e5
 t1 = (a[:, 3] - a[:, 2].min()) / 1e5
-hw, xcc = a[:, 0], a[:, 1]
+hw, xcc = a[:, 0], a[:, 1] >> 28
 key = ((xcc & 7) << 10) | (((hw >> 13) & 7) << 7) | (((hw >> 12) & 1) << 6) | (((hw >> 8) & 15) << 2) | ((hw >> 4) & 3)
 d = collections.defaultdict(list)
 for i in range(len(a)):
