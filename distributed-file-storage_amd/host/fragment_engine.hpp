@@ -141,6 +141,56 @@ public:
         return res;
     }
 
+    // sendFragmentsToPeers + buildFragmentsJson (SN:195-205, 629-642): the
+    // storeFragments body for every peer k != uploader (0-based, ascending),
+    // built on the device with the Base64 encoded straight into it.
+    std::vector<std::string> storeBodies(const Bytes& file, const std::string& fileId, int parts, int uploader) {
+        dfs_span sp{0, file.size()};
+        const Bytes dig = unhex(fileId);
+        std::vector<uint64_t> off(parts);
+        check(dfs_store_bodies_build(ctx_, nullptr, &sp, 1, parts, uploader, dig.data(), nullptr, off.data(), 0),
+              "buildFragmentsJson (layout)");
+        std::string buf(off[parts - 1] ? off[parts - 1] : 1, '\0');
+        check(dfs_store_bodies_build(ctx_, file.empty() ? nullptr : file.data(), &sp, 1, parts, uploader, dig.data(),
+                                     &buf[0], off.data(), 0),
+              "buildFragmentsJson");
+        std::vector<std::string> bodies;
+        for (int k = 0, j = 0; k < parts; ++k) {
+            if (k == uploader) continue;
+            bodies.push_back(buf.substr(off[j++], dfs_store_body_len(file.size(), parts, k, (k + 1) % parts)));
+        }
+        return bodies;
+    }
+
+    // handleInternalStoreFragments (SN:265-293) for a body in
+    // buildFragmentsJson form, parsed on the device: fileId and index ->
+    // (data, hash), in body order.  Returns false for a body in any other
+    // form (DFS_E_WIRE: the caller parses it with parseJson); throws
+    // IllegalArgumentException where Base64.getDecoder().decode would.
+    bool receiveStoreBody(const std::string& body, std::string& fileId,
+                          std::vector<std::pair<int, std::pair<Bytes, std::string>>>& frags) {
+        dfs_span sp{0, body.size()};
+        std::vector<uint64_t> out_off(2), foff(2), flen(2);
+        Bytes out(3 * ((body.size() + 3) / 4) + 1);
+        uint32_t idx[2];
+        uint8_t dig[64];
+        char ids[64];
+        int32_t st = 0;
+        check(dfs_store_bodies_receive(ctx_, body.data(), &sp, 1, out.data(), out_off.data(), idx, foff.data(),
+                                       flen.data(), dig, ids, &st, 0),
+              "handleInternalStoreFragments");
+        if (st == DFS_E_WIRE) return false;
+        fileId.assign(ids, 64);
+        frags.clear();
+        for (int q = 0; q < 2; ++q) {
+            if (st == DFS_E_DECODE && flen[q] == 0 && q == 1) break;
+            frags.push_back({static_cast<int>(idx[q]),
+                             {Bytes(out.begin() + foff[q], out.begin() + foff[q] + flen[q]), hex(dig + 32 * q)}});
+        }
+        if (st == DFS_E_DECODE) throw IllegalArgumentException("Illegal base64 character");
+        return true;
+    }
+
     // handleDownload's ordered gather + verify (SN:419-458).  frags[i] is
     // the fragment i found locally or fetched, or nullopt.
     Bytes reassembleAndVerify(const std::string& fileId, const std::vector<std::optional<Bytes>>& frags) {

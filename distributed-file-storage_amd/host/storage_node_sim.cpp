@@ -93,9 +93,18 @@ struct Cluster {
     std::map<int, std::string> storeFragments(int id, const std::string& body) {
         Node& n = node(id);
         if (!n.up) throw std::runtime_error("Connection refused");
-        auto parsed = parseJson(body);
-        auto got = eng.storeFragments(parsed.second);
         std::map<int, std::string> resp;
+        std::string fileId;
+        std::vector<std::pair<int, std::pair<dfs::Bytes, std::string>>> dev;
+        if (eng.receiveStoreBody(body, fileId, dev)) {  // device parse + decode + hash
+            for (auto& kv : dev) {
+                n.fragments[fileId][kv.first] = kv.second.first;  // Files.write(<i>.frag), SN:284-285
+                resp[kv.first] = kv.second.second;
+            }
+            return resp;
+        }
+        auto parsed = parseJson(body);  // any other body form: the reference's parser
+        auto got = eng.storeFragments(parsed.second);
         for (auto& kv : got) {
             n.fragments[parsed.first][kv.first] = kv.second.first;  // Files.write(<i>.frag), SN:284-285
             resp[kv.first] = kv.second.second;
@@ -118,15 +127,18 @@ struct Cluster {
                 std::printf("[%d] Saved fragment %d locally\n", u, f.index);
             }
         }
-        // sendFragmentsToPeers (SN:195-224)
-        for (int k = 0; k < TOTAL_NODES; ++k) {
+        // sendFragmentsToPeers (SN:195-224); every peer's body built on the device
+        const std::vector<std::string> bodies = eng.storeBodies(file, fileId, TOTAL_NODES, u0);
+        for (int k = 0, j = 0; k < TOTAL_NODES; ++k) {
             if (k == u0) continue;
             const int f1 = k, f2 = (k + 1) % TOTAL_NODES;
             bool ok = false;
             for (int attempt = 1; attempt <= 3 && !ok; ++attempt) {
                 std::printf("[%d] Sending fragments %d and %d to node %d (attempt %d)\n", u, f1, f2, k + 1, attempt);
                 try {
-                    const std::string body = dfs::buildFragmentsJson(fileId, {&up.second[f1], &up.second[f2]});
+                    const std::string& body = bodies[j];
+                    if (body != dfs::buildFragmentsJson(fileId, {&up.second[f1], &up.second[f2]}))
+                        throw std::logic_error("device body differs from buildFragmentsJson");
                     auto remote = storeFragments(k + 1, body);
                     ok = true;
                     for (int fi : {f1, f2}) {  // SN:250-257
@@ -143,6 +155,7 @@ struct Cluster {
                 std::printf("[%d] FAILED sending to node %d\n", u, k + 1);
                 return "";  // 500 "Replication failed", SN:174-177
             }
+            ++j;
         }
         const std::string manifest = dfs::buildManifestJson(fileId, name, TOTAL_NODES);
         for (auto& n : nodes) n.manifests[fileId] = manifest;  // save + announce (SN:180-186)
