@@ -18,6 +18,11 @@ Extra objects on the line:
   roofline_b64  the Base64 encode kernel vs the HBM peak
   cpu_baseline  CPU restatement (OpenSSL SHA-NI SHA-256 + scalar Base64, one
                 file per thread) on a bounded sample, rank 0, N = 1 only
+  download      handleDownload over the same files: Base64 decode into place +
+                fragment / fileId SHA-256 verify, and the raw-fragment gather
+  wire          storeFragments request bodies built on the device, then
+                received (parse + decode + SHA-256) on the device
+  replication   N > 1: ring and all-to-all placement over RCCL, degraded read
 """
 from __future__ import annotations
 
@@ -78,13 +83,18 @@ def parse():
     ap.add_argument("--dl-steps", type=int, default=2)
     ap.add_argument("--wire-files", type=int, default=16384, help="files in the storeFragments body leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the storeFragments body leg")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4),
-                    help="2: BASELINE configs[1] (default bench line); 4: configs[3], the long-fragment skew "
-                         "(1,024 x 256 MiB, N=5) streamed through HBM in chunks, its own JSON line")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
+                    help="2: BASELINE configs[1] (default bench line); 3: configs[2]'s per-GPU shard "
+                         "(131,072 x 256 KiB, N=8 per GPU; 1M files on 8 GPUs); 4: configs[3], the long-fragment "
+                         "skew (1,024 x 256 MiB, N=5) streamed through HBM in chunks, its own JSON line")
     ap.add_argument("--long-files", type=int, default=1024)
     ap.add_argument("--long-size", type=int, default=256 << 20)
     ap.add_argument("--long-chunk", type=int, default=192 * 87381, help="bytes per file per chunk (x192)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config == 3:  # BASELINE configs[2]: 1M files x 256 KiB sharded by file over 8 GPUs, N = 8
+        args.files, args.file_size, args.nfrag = 131072, 256 << 10, 8
+        args.wire_files = min(args.wire_files, 65536)
+    return args
 
 
 def cpu_baseline(args, log):
@@ -108,12 +118,17 @@ def cpu_baseline(args, log):
     secs, _, _ = O.cpu_upload_bench(nfiles, S, N, threads, use_openssl=(kind_sha == "openssl"))
     gbs = nfiles * S / secs / 1e9
     log(f"cpu baseline: {nfiles} files x {S} B on {threads} threads: {secs:.2f} s -> {gbs:.3f} GB/s")
+    # one connection-handler thread alone (1-thread and all-core)
+    n1 = int(max(1, min(20000, 3.0 / per_file)))
+    secs1, _, _ = O.cpu_upload_bench(n1, S, N, 1, use_openssl=(kind_sha == "openssl"))
+    gbs1 = n1 * S / secs1 / 1e9
+    log(f"cpu baseline: {n1} files on 1 thread: {secs1:.2f} s -> {gbs1:.3f} GB/s")
     return {"value": round(gbs, 4), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"{nfiles} synthetic files x {S} B, N={N}: fileId + fragment SHA-256 "
                       f"({'OpenSSL SHA256 (SHA-NI), approximating HotSpot intrinsic' if kind_sha == 'openssl' else 'scalar C'})"
                       f" + scalar Base64, one file per thread (thread-per-connection, SN:30); "
                       f"CPU proxy, not Java (no JDK on the box)",
-            "seconds": round(secs, 3)}
+            "seconds": round(secs, 3), "single_thread_value": round(gbs1, 4), "single_thread_files": n1}
 
 
 def replication_leg(args, eng, files, S, N, dev, log):

@@ -97,6 +97,45 @@ def test_b64_decode_alignments_and_lengths(engine):
                 assert g == d
 
 
+def test_b64_decode_multitile_every_output_phase(engine):
+    """The LDS-staged decode (tiles of 16 KiB of chars, 16-byte aligned output
+    chunks cut at byte offset h mod 3): messages spanning 1-5 tiles at every
+    output address mod 16 and every input address mod 4, incl. lengths that
+    end one char before / after a tile and every final-unit form."""
+    rng = np.random.default_rng(23)
+    sizes = [12287, 12288, 12289, 24575, 24576, 24577, 49150, 61441, 65536 + 7]
+    datas = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in sizes]
+    texts = [base64.b64encode(d) for d in datas]
+    texts += [t.rstrip(b"=") for t in texts]  # unpadded final units decode too (JDK basic decoder)
+    datas += datas
+    for pad_in in (0, 1, 2, 3):
+        buf = np.frombuffer(b"".join(b"#" * pad_in + t for t in texts), dtype=np.uint8).copy()
+        spans, p = [], 0
+        for t in texts:
+            spans.append((p + pad_in, len(t)))
+            p += len(t) + pad_in
+        for out_phase in range(16):
+            offs, o = [], out_phase
+            for d in datas:
+                offs.append(o)
+                o += (len(d) + 16 + 15) // 16 * 16 + out_phase
+            got = _decode_spans(engine, buf, spans, offs)
+            for d, g in zip(datas, got):
+                assert g == d, (pad_in, out_phase, len(d))
+
+
+def test_reassemble_multitile_every_alignment(engine):
+    """gather_kernel: fragments of 16 KiB tiles and more, every destination
+    phase mod 16 (via the file size mod 16 shifting later fragments) and
+    every source phase (host fragments are staged back to back)."""
+    files = [O.c_synth(40 + k, 0, 5 * 16384 * 3 + k) for k in range(16)] + [O.c_synth(60, 0, 1 << 20)]
+    ups = engine.upload(files, 5)
+    frags = [[d[g.offset:g.offset + g.length] for g in u.fragments] for d, u in zip(files, ups)]
+    res = engine.reassemble_verify(frags, [u.file_id for u in ups])
+    for d, (st, body, h) in zip(files, res):
+        assert st == 0 and body == d and h == hashlib.sha256(d).hexdigest()
+
+
 def _decode_spans(engine, buf, spans, out_off):
     import ctypes
     n = len(spans)
