@@ -232,21 +232,27 @@ __device__ __forceinline__ uint32_t dec_unit_bytes(const uint8_t* __restrict__ l
     return (d0 << 18) | (d1 << 12) | (d2 << 6) | d3;
 }
 
-// Tail item of one message: validates the body units no main item owns,
-// decodes the final unit, writes the head and tail bytes and sets status /
-// out_len (SN:281's IllegalArgumentException cases).
+// Tail step of one message, run by the 64 lanes of one wave: validates the
+// body units no tile owns (at most 8: before u_first and after the last whole
+// group), decodes the final unit (every lane, same address: a broadcast
+// load), writes the head bytes [0, h) and tail bytes [h + 16 nchunks, total)
+// — at most 15 + 28, one byte per lane, all loads in flight at once — and
+// sets status / out_len (SN:281's IllegalArgumentException cases, DESIGN.md
+// §3.2).
 __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const StreamJob& job, const DecGeom& G,
                                       const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                       int32_t* __restrict__ status, uint64_t* __restrict__ out_len) {
+    const uint32_t lane = threadIdx.x & 63u;
     const uint64_t L = job.len;
-    uint32_t bad = 0;
     const uint32_t r = static_cast<uint32_t>(L & 3u);
     bool err = (r == 1u);
+    // Units outside the tiles: [0, u_first) and [covered_end, body_units).
     const uint64_t covered_end = G.u_first + 4 * G.ng;
-    for (uint64_t u = 0; u < G.body_units; ++u) {
-        if (u >= G.u_first && u < covered_end) { u = covered_end - 1; continue; }
-        dec_unit_bytes(lut, src, u, bad);
-    }
+    const uint64_t head_units = G.u_first < G.body_units ? G.u_first : G.body_units;
+    const uint64_t u = lane < head_units ? lane : covered_end + (lane - head_units);
+    uint32_t bad = 0;
+    if (u < G.body_units && (lane < head_units || u >= covered_end)) dec_unit_bytes(lut, src, u, bad);
+    if (__ballot((bad & 0x80u) != 0)) err = true;
     uint32_t fin_bytes = 0, fin_val = 0;
     if (!err && L) {
         const uint64_t f = 4 * G.body_units;  // first char of the final unit
@@ -267,27 +273,25 @@ __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const 
             fin_val = (d0 << 18) | (d1 << 12) | (d2 << 6);
         }
     }
-    if (bad & 0x80u) err = true;
     const uint64_t total = err ? 0 : G.nb + fin_bytes;
     if (!err) {
-        // Head bytes [0, min(h, nb)) and tail bytes [h + 12nc, total).
-        auto byte_at = [&](uint64_t i) -> uint8_t {
-            const uint64_t u = i / 3;
-            uint32_t b2 = 0;
-            const uint32_t v = (u < G.body_units) ? dec_unit_bytes(lut, src, u, b2) : fin_val;
-            return static_cast<uint8_t>(v >> (16 - 8 * static_cast<uint32_t>(i % 3)));
-        };
+        // Lane i < 16: head byte i; lane i >= 16: tail byte tail_start + i - 16.
         const uint64_t head_end = G.h < total ? G.h : total;
-        for (uint64_t i = 0; i < head_end; ++i) dst[i] = byte_at(i);
-        for (uint64_t i = G.h + 16 * G.nchunks; i < total; ++i) {
-            if (i < head_end) continue;
-            dst[i] = byte_at(i);
+        const uint64_t tail_start = G.h + 16 * G.nchunks > head_end ? G.h + 16 * G.nchunks : head_end;
+        const uint64_t i = lane < 16 ? lane : tail_start + (lane - 16);
+        if (lane < 16 ? i < head_end : i < total) {
+            const uint64_t q = i / 3;
+            uint32_t b2 = 0;
+            const uint32_t v = (q < G.body_units) ? dec_unit_bytes(lut, src, q, b2) : fin_val;
+            dst[i] = static_cast<uint8_t>(v >> (16 - 8 * static_cast<uint32_t>(i % 3)));
         }
     }
-    int32_t flags = err ? 1 : 0;
-    if (job.expect && !err && total + 1 != job.expect) flags |= 2;
-    if (flags) atomicOr(status + job.id, flags);
-    if (out_len) out_len[job.id] = total;
+    if (lane == 0) {
+        int32_t flags = err ? 1 : 0;
+        if (job.expect && !err && total + 1 != job.expect) flags |= 2;
+        if (flags) atomicOr(status + job.id, flags);
+        if (out_len) out_len[job.id] = total;
+    }
 }
 
 // One tile = kDecGroupsPerTile 4-unit groups (16 KiB of chars) -> 12 KiB of
@@ -298,7 +302,7 @@ __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const 
 // 256i + l (i < 3) out of the decoded stream at byte offset e and writes
 // each with one dwordx4 store at a 16-byte aligned address (a wave writes
 // 1 KiB contiguous per instruction).  Head, tail and final unit: dec_tail,
-// on one lane of the message's last tile.  NT bit 0 = non-temporal stores,
+// on wave 0 of the message's last tile.  NT bit 0 = non-temporal stores,
 // bit 1 = non-temporal loads.
 template <int NT>
 __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
@@ -377,7 +381,7 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
                 else *d = o;
             }
         }
-        if (threadIdx.x == 0 && t + 1 == jobs[j + 1].tile_start)  // the message's last tile
+        if (threadIdx.x < 64 && t + 1 == jobs[j + 1].tile_start)  // wave 0 of the message's last tile
             dec_tail(lut, jobs[j], G, src, dst, status, out_len);
         __syncthreads();  // stream[] is rewritten by the next tile
     }
