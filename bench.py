@@ -73,6 +73,7 @@ def parse():
     ap.add_argument("--align128", action=argparse.BooleanOptionalAction, default=True,
                     help="DFS_LAYOUT_ALIGN128: every fragment's Base64 starts on a 128-byte boundary")
     ap.add_argument("--b64-steps", type=int, default=3, help="steps of the standalone Base64 leg")
+    ap.add_argument("--frag-only-steps", type=int, default=3, help="steps of the fragment-only (no fileId) leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     ap.add_argument("--verify", type=int, default=8, help="files spot-checked against the oracle (rank 0)")
@@ -514,6 +515,22 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    # ---- fragment-only variant: the same step without the fileId
+    # SHA-256 (SN:127), e.g. for a caller that already knows the content address.
+    frag_only = None
+    if args.frag_only_steps:
+        eng.set_profiling(True)
+        fo_ms, fo_sha = [], []
+        for _ in range(args.frag_only_steps):
+            plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), flags | dfs_amd.DFS_NO_FILEID)
+            t = eng.timings()
+            fo_ms.append(t["total"]); fo_sha.append(t["sha"])
+        eng.set_profiling(False)
+        fo = float(np.mean(fo_ms))
+        frag_only = {"ms_per_step": round(fo, 3), "gbps": round(F * S / (fo / 1e3) / 1e9, 3),
+                     "sha_ms": round(float(np.mean(fo_sha)), 3),
+                     "note": "fragment SHA-256 + Base64 only (no fileId SHA-256), HIP-event device time, this GPU"}
+
     # ---- the HBM-bound Base64 encode pass alone (roofline_b64) -----------------
     # Outside the timed steps (in the default fused mode the upload writes the
     # Base64 from the SHA kernel); same plan, same buffers, own HIP events.
@@ -596,6 +613,8 @@ def main():
                                  "the timed steps"},
         "verified": ok,
     }
+    if frag_only:
+        result["fragment_only"] = frag_only
     if not args.no_download:
         try:
             result["download"] = download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log)
