@@ -294,8 +294,8 @@ __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const 
     }
 }
 
-// One tile = kDecGroupsPerTile 4-unit groups (16 KiB of chars) -> 12 KiB of
-// output.  Phase 1: lane l loads groups 256i + l (i < 4) with one dwordx4
+// One tile = GPL x 256 4-unit groups (GPL = 4: 16 KiB of chars -> 12 KiB of
+// output).  Phase 1: lane l loads groups 256i + l (i < GPL) with one dwordx4
 // each (a wave reads 1 KiB contiguous per instruction, all four loads in
 // flight), decodes them through the LDS alphabet and parks the 12 bytes of
 // each at LDS offset 12 * group.  Phase 2: lane l cuts 16-byte output chunks
@@ -304,15 +304,17 @@ __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const 
 // 1 KiB contiguous per instruction).  Head, tail and final unit: dec_tail,
 // on wave 0 of the message's last tile.  NT bit 0 = non-temporal stores,
 // bit 1 = non-temporal loads.
-template <int NT>
+template <int NT, int GPL>
 __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
                                                                   uint8_t* __restrict__ out,
                                                                   int32_t* __restrict__ status,
                                                                   uint64_t* __restrict__ out_len) {
+    constexpr uint32_t kGroups = GPL * kStreamBlock;  // 4-unit groups per tile
+    constexpr uint32_t kChunks = 3 * GPL * 64;        // 16-byte output chunks per tile (12 kGroups / 16)
     __shared__ uint8_t lut[256];
-    __shared__ uint32_t stream[kDecGroupsPerTile * 3 + 4];  // decoded bytes of the tile (+1 unit)
+    __shared__ uint32_t stream[kGroups * 3 + 4];  // decoded bytes of the tile (+1 unit)
     build_dec_lut(lut);
     __syncthreads();
 
@@ -327,12 +329,12 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
         const DecGeom G = dec_geom(jobs[j].len, reinterpret_cast<uintptr_t>(dst));
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
         const uint64_t k = t - jobs[j].tile_start;
-        const uint64_t g0 = k * kDecGroupsPerTile;  // first group of the tile
+        const uint64_t g0 = k * kGroups;  // first group of the tile
         // Group g's chars start at unit u_first + 4g, i.e. dword w0 + 4g.
         const uint32_t* w0 = reinterpret_cast<const uint32_t*>(src + 4 * G.u_first - sa);
-        uint32_t raw[4][5];
+        uint32_t raw[GPL][5];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < GPL; ++i) {
             const uint64_t g = g0 + threadIdx.x + static_cast<uint64_t>(i) * kStreamBlock;
             raw[i][0] = raw[i][1] = raw[i][2] = raw[i][3] = raw[i][4] = 0u;
             if (g < G.ng) {
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
         }
         uint32_t bad = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < GPL; ++i) {
             const uint32_t gl = threadIdx.x + static_cast<uint32_t>(i) * kStreamBlock;  // group in the tile
             if (g0 + gl < G.ng) {
                 uint32_t v[4];
@@ -360,18 +362,18 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
         // The tile's last chunk reaches e bytes into the next group's first
         // unit (a body unit whenever that chunk exists); its chars are
         // validated by the tile that owns it.
-        const uint64_t c0 = k * kDecChunksPerTile;  // first chunk of the tile
-        if (threadIdx.x == 0 && G.e && c0 + kDecChunksPerTile <= G.nchunks) {
+        const uint64_t c0 = k * kChunks;  // first chunk of the tile
+        if (threadIdx.x == 0 && G.e && c0 + kChunks <= G.nchunks) {
             uint32_t b2 = 0;
-            const uint32_t v = dec_unit_bytes(lut, src, G.u_first + 4 * (g0 + kDecGroupsPerTile), b2);
-            stream[3 * kDecGroupsPerTile] = __builtin_amdgcn_perm(0u, v, 0x0c000102u);
+            const uint32_t v = dec_unit_bytes(lut, src, G.u_first + 4 * (g0 + kGroups), b2);
+            stream[3 * kGroups] = __builtin_amdgcn_perm(0u, v, 0x0c000102u);
         }
         if (bad & 0x80u) atomicOr(status + jobs[j].id, 1);
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
+        for (int i = 0; i < (kChunks + kStreamBlock - 1) / kStreamBlock; ++i) {
             const uint32_t m = threadIdx.x + static_cast<uint32_t>(i) * kStreamBlock;  // chunk in the tile
-            if (c0 + m < G.nchunks) {
+            if ((kChunks % kStreamBlock == 0 || m < kChunks) && c0 + m < G.nchunks) {
                 const u32x4 a = *reinterpret_cast<const u32x4*>(stream + 4 * m);
                 const uint32_t n4 = G.e ? stream[4 * m + 4] : 0u;
                 const u32x4 o = u32x4{align_bytes(a.y, a.x, G.e), align_bytes(a.z, a.y, G.e),
@@ -412,16 +414,19 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 }
 
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                             int32_t* status, uint64_t* out_len, hipStream_t s, int nt) {
+                             int32_t* status, uint64_t* out_len, hipStream_t s, int nt, int gpl) {
     if (ntiles == 0) return hipSuccess;
     const dim3 g(stream_grid(ntiles)), b(kStreamBlock);
-#define DFS_DEC(N) hipLaunchKernelGGL((b64_decode_kernel<N>), g, b, 0, s, in, jobs, njobs, ntiles, out, status, out_len)
-    switch (nt & 3) {
-        case 0: DFS_DEC(0); break;
-        case 1: DFS_DEC(1); break;
-        case 2: DFS_DEC(2); break;
-        default: DFS_DEC(3); break;
+#define DFS_DEC(N, G) hipLaunchKernelGGL((b64_decode_kernel<N, G>), g, b, 0, s, in, jobs, njobs, ntiles, out, status, out_len)
+#define DFS_DEC_NT(G)                  \
+    switch (nt & 3) {                  \
+        case 0: DFS_DEC(0, G); break;  \
+        case 1: DFS_DEC(1, G); break;  \
+        case 2: DFS_DEC(2, G); break;  \
+        default: DFS_DEC(3, G); break; \
     }
+    if (gpl == 2) { DFS_DEC_NT(2) } else if (gpl == 4) { DFS_DEC_NT(4) } else { DFS_DEC_NT(8) }
+#undef DFS_DEC_NT
 #undef DFS_DEC
     return hipGetLastError();
 }

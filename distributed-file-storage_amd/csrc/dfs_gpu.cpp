@@ -68,6 +68,7 @@ struct dfs_ctx {
     int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
     int b64_nt = 3;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
     int dec_nt = 3;              // non-temporal decode: bit 0 stores, bit 1 loads (DFS_DEC_NT)
+    int dec_gpl = 8;             // decode: 4-unit groups per thread per tile, 2, 4 or 8 (DFS_DEC_GPL)
     bool b64_pair = true;        // 12-bit pair table (DFS_B64_LUT=12) vs 6-bit alphabet (=6)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
@@ -231,6 +232,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
     if (const char* w = std::getenv("DFS_B64_NT")) c->b64_nt = std::atoi(w) & 3;
     if (const char* w = std::getenv("DFS_DEC_NT")) c->dec_nt = std::atoi(w) & 3;
+    if (const char* w = std::getenv("DFS_DEC_GPL")) c->dec_gpl = std::atoi(w) == 2 ? 2 : std::atoi(w) == 4 ? 4 : 8;
     if (const char* w = std::getenv("DFS_B64_LUT")) c->b64_pair = std::atoi(w) != 6;
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     hipError_t e = hipSetDevice(device);
@@ -562,7 +564,7 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
         j.id = i;
         items[i] = dec_items(msgs[i].len, reinterpret_cast<uintptr_t>(d_out + out_off[i]));
     }
-    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecGroupsPerTile);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->dec_gpl) * dfs::kStreamBlock);
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * n));
     HIPC(c->buf[B_OUTLEN].ensure(8ull * n));
@@ -571,7 +573,7 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
     tm.begin(DFS_T_B64DEC, s);
     HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), n, ntiles, d_out,
                                 c->buf[B_STATUS].as<int32_t>(), c->buf[B_OUTLEN].as<uint64_t>(), s,
-                                c->dec_nt));
+                                c->dec_nt, c->dec_gpl));
     tm.end(DFS_T_B64DEC, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(n);
@@ -993,7 +995,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         sha.push_back(msg(file_off[f], file_len[f], nf + f));
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kDecGroupsPerTile);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->dec_gpl) * dfs::kStreamBlock);
     const uint32_t prio = sort_lanes(sha);  // one message per lane, persistent sha256_lanes
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
@@ -1004,7 +1006,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64DEC, s);
     HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out,
-                                c->buf[B_STATUS].as<int32_t>(), nullptr, s, c->dec_nt));
+                                c->buf[B_STATUS].as<int32_t>(), nullptr, s, c->dec_nt, c->dec_gpl));
     tm.end(DFS_T_B64DEC, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));

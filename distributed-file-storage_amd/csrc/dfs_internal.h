@@ -47,13 +47,11 @@ constexpr int kEncGroupsPerTile = 1024;  // 12-byte groups (4 per thread)
 // Base64 decode geometry of one message of L chars decoding to dst (shared
 // by the host's tile count and b64_decode_kernel).  q = L/4 full units, r =
 // L%4; the final unit (padded, or the r trailing chars) is decoded by the
-// tail step, the body_units before it by tiles of kDecGroupsPerTile 4-unit
+// tail step, the body_units before it by tiles of gpl x 256 4-unit
 // groups starting at unit u_first = h/3, where h = bytes up to the first
 // 16-byte aligned output address.  Main output = 16-byte chunks
 // [h + 16m, h + 16m + 16), m < nchunks, cut from the decoded stream of the
 // ng whole groups at byte offset e = h % 3.
-constexpr int kDecGroupsPerTile = 4 * kStreamBlock;  // 4 groups per thread
-constexpr int kDecChunksPerTile = 3 * kStreamBlock;  // 16-byte output chunks (3 per thread)
 constexpr int kCopyChunksPerTile = 1024; // gather: 16-byte output chunks (4 per thread)
 struct DecGeom {
     uint64_t body_units;
@@ -129,7 +127,8 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 // a different length sets status bit 2.  nt bit 0 = non-temporal stores,
 // bit 1 = non-temporal loads.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, int nt = 3);
+                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, int nt = 3,
+                             int gpl = 8);  // gpl: 4-unit groups per thread per tile (2, 4 or 8)
 // Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
 hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
                                    hipStream_t s);
