@@ -68,6 +68,7 @@ struct dfs_ctx {
     int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
     int b64_nt = 3;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
     int dec_nt = 3;              // non-temporal decode: bit 0 stores, bit 1 loads (DFS_DEC_NT)
+    int gather_per = 4;          // gather: 16-byte chunks per thread per tile, 4 or 8 (DFS_GATHER_PER)
     int dec_gpl = 8;             // decode: 4-unit groups per thread per tile, 2, 4 or 8 (DFS_DEC_GPL)
     bool b64_pair = true;        // 12-bit pair table (DFS_B64_LUT=12) vs 6-bit alphabet (=6)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
@@ -232,6 +233,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
     if (const char* w = std::getenv("DFS_B64_NT")) c->b64_nt = std::atoi(w) & 3;
     if (const char* w = std::getenv("DFS_DEC_NT")) c->dec_nt = std::atoi(w) & 3;
+    if (const char* w = std::getenv("DFS_GATHER_PER")) c->gather_per = std::atoi(w) == 8 ? 8 : 4;
     if (const char* w = std::getenv("DFS_DEC_GPL")) c->dec_gpl = std::atoi(w) == 2 ? 2 : std::atoi(w) == 4 ? 4 : 8;
     if (const char* w = std::getenv("DFS_B64_LUT")) c->b64_pair = std::atoi(w) != 6;
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
@@ -910,7 +912,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
         sha.push_back(msg(file_off[f], flen[f], f));  // SN:454
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, dfs::kCopyChunksPerTile);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->gather_per) * dfs::kStreamBlock);
     const uint32_t prio = sort_lanes(sha);
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
@@ -918,7 +920,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_GATHER, s);
-    HIPC(dfs::launch_gather(c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s));
+    HIPC(dfs::launch_gather(c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s, c->gather_per));
     tm.end(DFS_T_GATHER, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));

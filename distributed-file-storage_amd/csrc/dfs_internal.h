@@ -52,7 +52,6 @@ constexpr int kEncGroupsPerTile = 1024;  // 12-byte groups (4 per thread)
 // 16-byte aligned output address.  Main output = 16-byte chunks
 // [h + 16m, h + 16m + 16), m < nchunks, cut from the decoded stream of the
 // ng whole groups at byte offset e = h % 3.
-constexpr int kCopyChunksPerTile = 1024; // gather: 16-byte output chunks (4 per thread)
 struct DecGeom {
     uint64_t body_units;
     uint64_t nb;       // body bytes
@@ -136,9 +135,10 @@ hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const ui
 // 64 fileId chars of body k go to file_ids + 64k.
 hipError_t launch_store_body_parse(const char* in, const uint64_t* spans, uint32_t n, BodyParse* out,
                                    char* file_ids, hipStream_t s);
-// Gather: job.src_off is an absolute device address of the fragment.
+// Gather: job.src_off is an absolute device address of the fragment; tiles
+// of per x 256 16-byte chunks (per = 4 or 8).
 hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                         hipStream_t s);
+                         hipStream_t s, int per = 4);
 hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
                         hipStream_t s, uint64_t file_off);
 // Compare n digests a[i] vs b[i] (32 B each); status[i*stride] = code if different.

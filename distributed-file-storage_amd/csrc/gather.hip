@@ -10,7 +10,7 @@
 namespace dfs {
 namespace {
 
-// Tile = kCopyChunksPerTile 16-byte output chunks: chunk c of a fragment
+// Tile = P x 256 16-byte output chunks: chunk c of a fragment
 // covers dst bytes [h + 16c, h + 16c + 16), a 16-byte aligned span (h = bytes
 // up to the first 16-aligned address, copy_items in dfs_gpu.cpp).  Every lane
 // issues the loads of all its chunks (dwordx4 + one dword when the source is
@@ -20,9 +20,9 @@ namespace {
 // byte is touched once.
 typedef uint32_t g32x4 __attribute__((ext_vector_type(4)));
 
+template <int P>  // 16-byte chunks per thread per tile
 __global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* __restrict__ jobs, uint32_t njobs,
                                                               uint64_t ntiles, uint8_t* __restrict__ out) {
-    constexpr int P = kCopyChunksPerTile / kStreamBlock;
     uint64_t t0, t1;
     tile_range(ntiles, t0, t1);
     if (t0 >= t1) return;
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* _
         const uint64_t nc = len > h ? (len - h) / 16 : 0;
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src + h)) & 3u;
         const uint32_t* w0 = reinterpret_cast<const uint32_t*>(src + h - sa);
-        const uint64_t c0 = (t - jobs[j].tile_start) * kCopyChunksPerTile + threadIdx.x;
+        const uint64_t c0 = (t - jobs[j].tile_start) * (P * kStreamBlock) + threadIdx.x;
         g32x4 v[P];
         uint32_t x[P];
 #pragma unroll
@@ -122,9 +122,13 @@ __global__ void digest_compare_kernel(const uint8_t* __restrict__ a, const uint8
 
 }  // namespace
 
-hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s) {
+hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s,
+                         int per) {
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
+    if (per == 8)
+        hipLaunchKernelGGL(gather_kernel<8>, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
+    else
+        hipLaunchKernelGGL(gather_kernel<4>, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
     return hipGetLastError();
 }
 
