@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -129,7 +130,31 @@ ShaDesc msg(uint64_t off, uint64_t len, uint64_t out) { return ShaDesc{off, len,
 // Sort SHA lanes longest-first (uniform waves) and count the lanes that
 // carry the long chains: those waves get issue priority in the kernel.
 uint32_t sort_lanes(std::vector<ShaDesc>& d) {
-    std::stable_sort(d.begin(), d.end(), [](const ShaDesc& a, const ShaDesc& b) { return a.len > b.len; });
+    // Longest first, stable.  Batches hold few distinct lengths (N fragment
+    // sizes + file sizes), so a counting sort over the distinct lengths is
+    // O(n); many distinct lengths fall back to a comparison sort.
+    std::vector<uint64_t> lens;
+    for (const ShaDesc& x : d) {
+        if (std::find(lens.begin(), lens.end(), x.len) == lens.end()) {
+            lens.push_back(x.len);
+            if (lens.size() > 32) break;
+        }
+    }
+    if (lens.size() <= 32) {
+        std::sort(lens.begin(), lens.end(), std::greater<uint64_t>());
+        std::vector<size_t> start(lens.size() + 1, 0);
+        std::vector<uint32_t> bucket(d.size());
+        for (size_t i = 0; i < d.size(); ++i) {
+            bucket[i] = static_cast<uint32_t>(std::find(lens.begin(), lens.end(), d[i].len) - lens.begin());
+            ++start[bucket[i] + 1];
+        }
+        for (size_t b = 0; b < lens.size(); ++b) start[b + 1] += start[b];
+        std::vector<ShaDesc> out(d.size());
+        for (size_t i = 0; i < d.size(); ++i) out[start[bucket[i]]++] = d[i];
+        d.swap(out);
+    } else {
+        std::stable_sort(d.begin(), d.end(), [](const ShaDesc& a, const ShaDesc& b) { return a.len > b.len; });
+    }
     if (d.size() < 2) return 0;
     const uint64_t med = d[d.size() / 2].len;
     uint32_t n = 0;
