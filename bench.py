@@ -626,6 +626,11 @@ def main():
         except Exception as e:
             result["wire"] = {"error": repr(e)[:300]}
     if world > 1 and not args.no_replicate:
+        # The upload's Base64 (91.6 GB at config 2) is not needed any more: free
+        # it so the placement buffers (held groups of every rank, all-to-all
+        # send / receive copies) fit beside the files in HBM.
+        b64 = None
+        torch.cuda.empty_cache()
         try:
             result["replication"] = replication_leg(args, eng, files, S, N, dev, log)
         except Exception as e:  # never lose the main line to the side measurement
