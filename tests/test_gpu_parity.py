@@ -98,7 +98,7 @@ def test_b64_decode_alignments_and_lengths(engine):
 
 
 def test_b64_decode_multitile_every_output_phase(engine):
-    """The LDS-staged decode (tiles of 16 KiB of chars, 16-byte aligned output
+    """The LDS-staged decode (tiles of 16 or 32 KiB of chars, 16-byte aligned output
     chunks cut at byte offset h mod 3): messages spanning 1-5 tiles at every
     output address mod 16 and every input address mod 4, incl. lengths that
     end one char before / after a tile and every final-unit form."""
@@ -505,3 +505,42 @@ def test_storage_node_sim_config1(golden):
                 me, e["name"], e["fileId"], ",".join(plans[str(me)]), e["size"])
             assert want in lines, want
     assert "[1] Download with nodes 2,3 down -> 500 Could not retrieve fragment 2" in lines
+
+
+def test_concurrent_handlers_share_one_ctx(engine):
+    """StorageNode runs one thread per connection (SN:30) and the ABI promises
+    that one ctx serialises its calls: 8 threads upload / download / receive
+    through the same engine at once (ctypes drops the GIL), every result
+    bit-exact against the oracle."""
+    import threading
+    errors = []
+
+    def worker(k):
+        try:
+            rng = random.Random(100 + k)
+            for it in range(6):
+                files = [O.c_synth(1000 * k + it * 10 + j, 0, rng.randrange(0, 300_000)) for j in range(3)]
+                ups = engine.upload(files, 5)
+                fd, frd, b64, off = O.c_upload_batch(files, 5)
+                for f, u in enumerate(ups):
+                    assert u.file_id == fd[f].tobytes().hex()
+                    for i, g in enumerate(u.fragments):
+                        assert g.hash == frd[f, i].tobytes().hex()
+                        assert g.b64 == b64[int(off[f * 5 + i]):int(off[f * 5 + i + 1])]
+                res = engine.download([[g.b64 for g in u.fragments] for u in ups], [len(x) for x in files],
+                                      [[g.hash for g in u.fragments] for u in ups], [u.file_id for u in ups])
+                assert all(st == 0 and body == x for x, (st, body) in zip(files, res))
+                bodies = [b for _, b in engine.store_bodies(files[:1], 5, k % 5, [ups[0].file_id])[0]]
+                got = engine.store_receive(bodies)
+                assert all(st == 0 and fid == ups[0].file_id for st, fid, _ in got)
+        except Exception as e:  # reported below
+            import traceback
+            errors.append(traceback.format_exc())
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors[0]
+    assert not any(t.is_alive() for t in threads)
