@@ -22,6 +22,7 @@ Extra objects on the line:
                 fragment / fileId SHA-256 verify, and the raw-fragment gather
   wire          storeFragments request bodies built on the device, then
                 received (parse + decode + SHA-256) on the device
+  store         on-disk fragment store: node 1's fragments HBM -> disk -> HBM
   replication   N > 1: ring and all-to-all placement over RCCL, degraded read
 """
 from __future__ import annotations
@@ -84,6 +85,8 @@ def parse():
     ap.add_argument("--dl-steps", type=int, default=2)
     ap.add_argument("--wire-files", type=int, default=16384, help="files in the storeFragments body leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the storeFragments body leg")
+    ap.add_argument("--store-files", type=int, default=2048, help="files in the on-disk fragment store leg")
+    ap.add_argument("--no-store", action="store_true", help="skip the on-disk fragment store leg")
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
                     help="2: BASELINE configs[1] (default bench line); 3: configs[2]'s per-GPU shard "
                          "(131,072 x 256 KiB, N=8 per GPU; 1M files on 8 GPUs); 4: configs[3], the long-fragment "
@@ -380,6 +383,57 @@ def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
                     "digests"}
 
 
+def store_leg(args, eng, files, fd, S, N, F, dev, log):
+    """On-disk fragment store (SN:147-166 upload save, SN:463-469 local load):
+    node 1 (0-based 0) keeps fragments {0, 1} of every sampled file; they go
+    HBM -> pinned ring -> <tmp>/node-1/<fileId>/fragments/<i>.frag and back
+    into HBM (dfs_store_write_fragments / dfs_store_read_fragments).  The
+    read follows the write, so it is a page-cache rate (the box gives no way
+    to drop caches).  Checked: every byte read back equals the file bytes."""
+    import shutil
+    import tempfile
+    import numpy as np
+    import torch
+    from dfs_amd.fragstore import FragmentStore, make_refs
+    R = min(F, args.store_files)
+    lens = split(S, N)
+    offs = [sum(lens[:i]) for i in range(N)]
+    keep = (0, 1)  # SN:143-145 for node 1
+    off = [f * S + offs[i] for f in range(R) for i in keep]
+    ln = [lens[i] for _ in range(R) for i in keep]
+    fi = [f for f in range(R) for _ in keep]
+    ix = [i for _ in range(R) for i in keep]
+    # fileId directory names: the upload's device-computed fileIds
+    dig = fd[:R * 32].view(R, 32).cpu().numpy()
+    tmp = tempfile.mkdtemp(prefix="dfs_store_")
+    try:
+        store = FragmentStore(1, tmp, engine=eng)
+        refs = make_refs(off, ln, fi, ix)
+        t0 = time.perf_counter()
+        st = store.write(dig, files.data_ptr(), refs, device=True)
+        t_w = time.perf_counter() - t0
+        total = int(sum(ln))
+        pos = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+        back = torch.empty(total, dtype=torch.uint8, device=dev)
+        rrefs = make_refs(pos, ln, fi, ix)
+        t0 = time.perf_counter()
+        st2, got = store.read(dig, back.data_ptr(), rrefs, device=True)
+        t_r = time.perf_counter() - t0
+        want = torch.cat([files[o:o + n] for o, n in zip(off, ln)])
+        ok = bool((st == 0).all()) and bool((st2 == 0).all()) and bool((got == np.array(ln)).all()) \
+            and bool(torch.equal(want, back))
+        del want, back
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    log(f"store: {2 * R} fragments, {total / 1e9:.2f} GB: write {t_w * 1e3:.0f} ms, read {t_r * 1e3:.0f} ms, ok={ok}")
+    return {"files": R, "fragments": 2 * R, "bytes": total, "node": 1,
+            "write_ms": round(t_w * 1e3, 2), "write_gbs": round(total / t_w / 1e9, 2),
+            "read_ms": round(t_r * 1e3, 2), "read_gbs": round(total / t_r / 1e9, 2), "ok": ok,
+            "threads": int(os.environ.get("DFS_STORE_THREADS", "0")) or "min(16, cores)",
+            "note": "HBM -> pinned staging ring -> <tmp>/node-1/<fileId>/fragments/<i>.frag (raw bytes, "
+                    "SN:166) and back (SN:466); wall clock, page cache (no fsync, as Files.write)"}
+
+
 def long_leg(args):
     """BASELINE configs[3]: files larger than HBM (dfs_amd.streaming).  Every
     chunk: synthesize the files' window on device (stands for bytes arriving
@@ -625,6 +679,11 @@ def main():
             result["wire"] = wire_leg(args, eng, files, fd, frd, S, N, F, dev, log)
         except Exception as e:
             result["wire"] = {"error": repr(e)[:300]}
+    if not args.no_store:
+        try:
+            result["store"] = store_leg(args, eng, files, fd, S, N, F, dev, log)
+        except Exception as e:
+            result["store"] = {"error": repr(e)[:300]}
     if world > 1 and not args.no_replicate:
         # The upload's Base64 (91.6 GB at config 2) is not needed any more: free
         # it so the placement buffers (held groups of every rank, all-to-all

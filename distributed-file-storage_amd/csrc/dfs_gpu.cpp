@@ -76,9 +76,17 @@ struct dfs_ctx {
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
     DevBuf buf[B_COUNT];
+    dfs::StoreStaging* store = nullptr;  // pinned staging ring of the fragment store
     std::mutex mu;
     hipStream_t stream() const { return user ? user : own; }
 };
+
+namespace dfs {
+hipStream_t ctx_stream(dfs_ctx* c) { return c->stream(); }
+int ctx_device(dfs_ctx* c) { return c->device; }
+std::mutex& ctx_mutex(dfs_ctx* c) { return c->mu; }
+StoreStaging*& ctx_store(dfs_ctx* c) { return c->store; }
+}  // namespace dfs
 
 struct dfs_upload_plan {
     int device = 0;
@@ -237,6 +245,7 @@ const char* dfs_strerror(int code) {
         case DFS_E_FRAG_MISMATCH: return "Hash mismatch on fragment";
         case DFS_E_NODEV: return "no gfx950 (MI355X) device available";
         case DFS_E_WIRE: return "storeFragments body not in buildFragmentsJson form (parse it with parseJson)";
+        case DFS_E_IO: return "fragment store I/O error (IOException)";
         default: return "unknown error";
     }
 }
@@ -280,6 +289,7 @@ int dfs_close(dfs_ctx* c) {
     if (c->own) (void)hipStreamSynchronize(c->own);
     if (c->aux) (void)hipStreamSynchronize(c->aux);
     for (auto& b : c->buf) b.release();
+    dfs::store_staging_free(c->store);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
     if (c->own) (void)hipStreamDestroy(c->own);

@@ -5,6 +5,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
+typedef struct dfs_ctx dfs_ctx;
+
 namespace dfs {
 
 // One SHA-256 lane: message bytes [off, off+len) of the batch buffer; the
@@ -144,5 +148,14 @@ hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uin
 // Compare n digests a[i] vs b[i] (32 B each); status[i*stride] = code if different.
 hipError_t launch_digest_compare(const uint8_t* a, const uint8_t* b, uint32_t n, int32_t code,
                                  int32_t* status, uint32_t status_div, hipStream_t s);
+
+// ctx internals for the on-disk fragment store (fragstore.cpp).  The store's
+// pinned staging ring lives in the ctx and is freed by dfs_close.
+struct StoreStaging;
+void store_staging_free(StoreStaging* s);
+hipStream_t ctx_stream(dfs_ctx* c);
+int ctx_device(dfs_ctx* c);
+std::mutex& ctx_mutex(dfs_ctx* c);
+StoreStaging*& ctx_store(dfs_ctx* c);
 
 }  // namespace dfs

@@ -26,6 +26,7 @@ DFS_E_CORRUPT = -6
 DFS_E_FRAG_MISMATCH = -7
 DFS_E_NODEV = -8
 DFS_E_WIRE = -9
+DFS_E_IO = -10
 
 DFS_DEVICE_PTRS = 0x1
 DFS_NO_FILEID = 0x2
@@ -44,6 +45,10 @@ DFS_T_SHA, DFS_T_B64ENC, DFS_T_B64DEC, DFS_T_GATHER, DFS_T_TOTAL, DFS_T_COUNT = 
 
 class dfs_span(ctypes.Structure):
     _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint64)]
+
+
+# dfs_frag_ref as a numpy record (24 bytes: off, len, file, index).
+FRAG_REF_DTYPE = [("off", "<u8"), ("len", "<u8"), ("file", "<u4"), ("index", "<u4")]
 
 
 _vp = ctypes.c_void_p
@@ -82,6 +87,8 @@ SIGNATURES = {
     "dfs_store_body_len": (_u64, [_u64, _u32, _u32, _u32]),
     "dfs_store_bodies_build": (_int, [_vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _u32]),
     "dfs_store_bodies_receive": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    "dfs_store_write_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _vp, _vp, _u32, _vp, _u32]),
+    "dfs_store_read_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _vp, _vp, _u32, _vp, _vp, _u32]),
 }
 
 _LIB = None

@@ -47,6 +47,8 @@ extern "C" {
 #define DFS_E_NODEV (-8)        /* no gfx950 device                               */
 #define DFS_E_WIRE (-9)         /* storeFragments body not in buildFragmentsJson  */
                                 /* form: the host parses it with parseJson        */
+#define DFS_E_IO (-10)          /* fragment store: Files.write / readAllBytes      */
+                                /* IOException (SN:166, 285, 466)                 */
 
 /* Flags. */
 #define DFS_DEVICE_PTRS 0x1u    /* data pointers are device pointers; async       */
@@ -259,6 +261,41 @@ int dfs_store_bodies_build(dfs_ctx* ctx, const uint8_t* files, const dfs_span* f
 int dfs_store_bodies_receive(dfs_ctx* ctx, const char* bodies, const dfs_span* body_spans, uint32_t n,
                              uint8_t* out, uint64_t* out_off, uint32_t* frag_index, uint64_t* frag_off,
                              uint64_t* frag_len, uint8_t* digests, char* file_ids, int32_t* status,
+                             uint32_t flags);
+
+/* ---- on-disk fragment store (SN:147-149, 163-166, 273-285, 463-469) ------ */
+/* A node's fragments live at
+ *   <node_root>/<fileId hex>/fragments/<index>.frag
+ * holding the raw fragment bytes (Files.write of the byte[] at SN:166 on
+ * upload and SN:285 on the replica receiver; read back by
+ * tryLoadFragmentLocal, SN:463-469).  node_root is the reference's dataRoot,
+ * data/node-<id> (SN:20).  The manifest.json beside them is not written here.
+ *   file_digest  host memory, 32 raw bytes per file; the directory name is
+ *                its lowercase hex (sha256Hex, SN:607-609)
+ *   refs[i]      fragment i: bytes data + off, len of them (read: capacity),
+ *                of file refs[i].file, fragment number refs[i].index
+ *   status[i]    0, DFS_E_IO (write / read failed), DFS_E_MISSING (read:
+ *                no such file, tryLoadFragmentLocal returns null) or
+ *                DFS_E_ARG (read: the file is longer than len)
+ * Directories are created as Files.createDirectories does (SN:149, 275);
+ * files are created or truncated (Files.write's default options).  With
+ * DFS_DEVICE_PTRS `data` is device memory: the bytes move through the ctx's
+ * pinned staging ring (HBM <-> host on the ctx stream, overlapped with the
+ * file I/O of a host thread pool).  Without it `data` is host memory and
+ * ctx may be NULL (pure file I/O).  Returns DFS_OK or the first failing
+ * status; every ref is attempted.  Synchronous. */
+typedef struct dfs_frag_ref {
+    uint64_t off;
+    uint64_t len;
+    uint32_t file;
+    uint32_t index;
+} dfs_frag_ref;
+int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest,
+                              const uint8_t* data, const dfs_frag_ref* refs, uint32_t n, int32_t* status,
+                              uint32_t flags);
+/* out_len[i] = bytes of fragment i (the file's size) when status[i] is 0. */
+int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, uint8_t* data,
+                             const dfs_frag_ref* refs, uint32_t n, uint64_t* out_len, int32_t* status,
                              uint32_t flags);
 
 /* ---- prepared upload (descriptor build once, run many; device pointers) --- */

@@ -422,3 +422,39 @@ def py_store_fragments(body: bytes):
             return "IllegalArgumentException", file_id, done, None
         done.append((index, data, py_sha256_hex(data)))
     return None, file_id, done, py_build_hash_response(file_id, [(i, h) for i, _, h in done])
+
+
+# ---- on-disk fragment store (SN:20, 147-149, 163-166, 273-285, 463-469) ----
+def py_fragment_path(data_root: str, file_id: str, index: int) -> str:
+    """dataRoot.resolve(fileId).resolve("fragments").resolve(i + ".frag")
+    (SN:147-148, 165, 464); dataRoot = data/node-<id> (SN:20)."""
+    return os.path.join(data_root, file_id, "fragments", f"{index}.frag")
+
+
+def py_store_write(data_root: str, file_id: str, index: int, data: bytes) -> None:
+    """Files.createDirectories(fragmentsDir) + Files.write(fragPath, fragment)
+    (SN:149, 166; 275, 285): create or truncate, raw bytes."""
+    path = py_fragment_path(data_root, file_id, index)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "wb") as f:
+        f.write(data)
+
+
+def py_try_load_fragment_local(data_root: str, file_id: str, index: int) -> Optional[bytes]:
+    """tryLoadFragmentLocal (SN:463-469): the bytes, or None if absent."""
+    path = py_fragment_path(data_root, file_id, index)
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def py_tree(root: str) -> dict:
+    """{relative path: bytes} of every file under root (tree comparison)."""
+    out = {}
+    for d, _, names in os.walk(root):
+        for nm in names:
+            p = os.path.join(d, nm)
+            with open(p, "rb") as f:
+                out[os.path.relpath(p, root)] = f.read()
+    return out
