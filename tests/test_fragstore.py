@@ -157,3 +157,51 @@ def test_device_store_round_trip(tmp_path, monkeypatch, engine, slot_mb):
     st, ln = store.read(dig, d_back.data_ptr(), refs, device=True)
     assert (st == 0).all() and list(ln) == [len(b) for b in blobs]
     assert d_back.cpu().numpy().tobytes() == buf.tobytes()
+
+
+@pytest.mark.gpu
+def test_device_config1_download_from_disk(tmp_path, engine, example_bytes):
+    """BASELINE config 1 with the disk in the loop: node 1 uploads examples/*
+    (+ a 1 MiB file), every node stores its pair from HBM (SN:163-166,
+    284-285), node 3 goes down, node 1 downloads: local fragments from its
+    own store, the rest from the first live holder's store (SN:421-451),
+    read straight into HBM, then gather + fileId verify on the device
+    (SN:454-458)."""
+    import torch
+    from dfs_amd.engine import reassemble_device
+    N, down, me = 5, 2, 0
+    files = [example_bytes[n] for n in sorted(example_bytes)] + [O.c_synth(3, 0, 1 << 20)]
+    ups = engine.upload(files, N)
+    dig = np.frombuffer(b"".join(bytes.fromhex(u.file_id) for u in ups), dtype=np.uint8).reshape(-1, 32)
+    S = [len(x) for x in files]
+    base = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+    d_files = torch.from_numpy(np.frombuffer(b"".join(files), dtype=np.uint8).copy()).to("cuda:0")
+    spans = [O.py_split(s, N) for s in S]
+    stores = [FragmentStore(k + 1, str(tmp_path / "data"), engine=engine) for k in range(N)]
+    for k in range(N):
+        off, ln, fi, ix = [], [], [], []
+        for f in range(len(files)):
+            for i in O.py_node_fragments(k, N):
+                o, l = spans[f][i]
+                off.append(int(base[f]) + o), ln.append(l), fi.append(f), ix.append(i)
+        assert (stores[k].write(dig, d_files.data_ptr(), make_refs(off, ln, fi, ix), device=True) == 0).all()
+    # download plan (SN:421-451): local first, then holders in order, node `down` offline
+    d_frag = torch.zeros(sum(S) + 64, dtype=torch.uint8, device="cuda:0")
+    addr = np.zeros(len(files) * N, dtype=np.uint64)
+    flen = np.zeros(len(files) * N, dtype=np.uint64)
+    per_node = {}
+    for f in range(len(files)):
+        for i in range(N):
+            src = me if i in O.py_node_fragments(me, N) else next(h for h in O.py_fragment_holders(i, N) if h != down)
+            o, l = spans[f][i]
+            per_node.setdefault(src, []).append((int(base[f]) + o, l, f, i))
+            addr[f * N + i] = d_frag.data_ptr() + int(base[f]) + o
+            flen[f * N + i] = l
+    for src, items in per_node.items():
+        off, ln, fi, ix = zip(*items)
+        st, got = stores[src].read(dig, d_frag.data_ptr(), make_refs(off, ln, fi, ix), device=True)
+        assert (st == 0).all() and list(got) == list(ln)
+    d_out = torch.zeros(sum(S) + 64, dtype=torch.uint8, device="cuda:0")
+    st, fdig = reassemble_device(engine, addr, flen, len(files), N, d_out.data_ptr(), base, expected=dig)
+    assert (st == 0).all() and (fdig == dig).all()
+    assert d_out[:sum(S)].cpu().numpy().tobytes() == b"".join(files)
