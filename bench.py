@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--rep-steps", type=int, default=3)
     ap.add_argument("--no-download", action="store_true", help="skip the download/verify leg")
     ap.add_argument("--dl-steps", type=int, default=2)
+    ap.add_argument("--dl-chunks", type=int, default=0,
+                    help="> 0: also time the chunked 2-context download (slower: see DESIGN §9)")
     ap.add_argument("--wire-files", type=int, default=16384, help="files in the storeFragments body leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the storeFragments body leg")
     ap.add_argument("--store-files", type=int, default=2048, help="files in the on-disk fragment store leg")
@@ -258,6 +260,10 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
         ok = ok and bool((st == 0).all())
     eng.set_profiling(False)
     ok = ok and bool(torch.equal(out, files[:F * S]))
+    pipe = None
+    if args.dl_chunks > 0:
+        pipe = pipelined_download(args, eng, files, fd, frd, b64, msp, out, S, N, F, dev)
+        ok = ok and pipe.get("ok", False)
     # Raw-fragment reassembly (SN:419-451, fragments fetched as raw bytes,
     # :513-514): gather the fragments of every file (spans of the upload
     # buffer) into `out`, then the fileId re-verify (:454-458).
@@ -292,8 +298,61 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
             "decode_frac_hbm": round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "sha_ms": round(float(np.mean(sha)), 3),
             "gather_ms": round(gat_ms, 3), "gather_gbs": round(gat_gbs, 1),
-            "gather_frac_hbm": round(gat_gbs / HBM_PEAK_GBS, 4), "ok": ok,
+            "gather_frac_hbm": round(gat_gbs / HBM_PEAK_GBS, 4), "ok": ok, **({"pipelined": pipe} if pipe else {}),
             "note": "wall_ms includes host-side job planning per call; gbps = file bytes / device time"}
+
+
+def pipelined_download(args, eng, files, fd, frd, b64, msp, out, S, N, F, dev):
+    """Server-style download: the same F files as chunks over two contexts on
+    two host threads (two connection handlers, SN:30, sharing a GPU), so one
+    chunk's verify SHA-256 runs beside the next chunk's Base64 decode.  The
+    second thread starts with a half chunk so the two do not run in lockstep.
+    Wall clock over the whole set, host planning included."""
+    import threading
+    import numpy as np
+    import torch
+    import dfs_amd
+    from dfs_amd.engine import download_device
+    K = max(2, args.dl_chunks)
+    step = F // K
+    bounds = [0, step // 2] + [step // 2 + step * i for i in range(1, K)] + [F]
+    bounds = sorted(set(b for b in bounds if 0 <= b <= F))
+    chunks = list(zip(bounds[:-1], bounds[1:]))
+    file_len = np.full(F, S, dtype=np.uint64)
+    file_off = np.arange(F, dtype=np.uint64) * np.uint64(S)
+    eng2 = dfs_amd.FragmentEngine(dev.index or 0)
+    engines = [eng, eng2]
+    ok = [True]
+
+    def run(t):
+        for c, (a, b) in enumerate(chunks):
+            if c % 2 != t:
+                continue
+            st = download_device(engines[t], b64.data_ptr(), msp[a * N:b * N], b - a, N, file_len[a:b],
+                                 frd.data_ptr() + a * N * 32, fd.data_ptr() + a * 32, out.data_ptr(), file_off[a:b])
+            ok[0] = ok[0] and bool((st == 0).all())
+
+    def once():
+        ths = [threading.Thread(target=run, args=(t,)) for t in (0, 1)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        return time.perf_counter() - t0
+
+    try:
+        once()
+        out.zero_()
+        torch.cuda.synchronize(dev)
+        walls = [once() for _ in range(max(1, args.dl_steps))]
+        torch.cuda.synchronize(dev)
+        good = ok[0] and bool(torch.equal(out, files[:F * S]))
+    finally:
+        eng2.close()
+    ms = float(np.mean(walls)) * 1e3
+    return {"chunks": len(chunks), "contexts": 2, "wall_ms": round(ms, 3),
+            "gbps": round(F * S / (ms / 1e3) / 1e9, 2), "ok": good}
 
 
 def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
