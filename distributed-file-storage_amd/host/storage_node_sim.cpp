@@ -11,9 +11,17 @@
 // Log lines use the reference's formats (SN:125, 128, 136, 160, 167, 209) so
 // config 1's "diff fragment SHA-256s" is a grep + diff.
 //
+// Fragments are real files: every node's data/node-<id>/<fileId>/fragments/
+// <i>.frag (SN:20, 147-166, 273-285), written and read through the library's
+// fragment store (dfs_store_write_fragments / dfs_store_read_fragments).
+// The data directory is $DFS_SIM_DATA (kept), else a fresh /tmp directory
+// removed at exit.
+//
 // usage: storage_node_sim <file>...   (prints the log to stdout; exit 0 = all
 //        downloads verified bit-exact)
 #include <cstdio>
+#include <cstdlib>
+#include <filesystem>
 #include <fstream>
 #include <iterator>
 #include <map>
@@ -28,6 +36,7 @@
 namespace {
 
 constexpr int TOTAL_NODES = 5;  // SN:15
+namespace fs = std::filesystem;
 
 std::string basename_of(const std::string& p) {
     const size_t s = p.find_last_of('/');
@@ -70,20 +79,55 @@ std::pair<std::string, std::vector<std::pair<int, std::string>>> parseJson(const
     return {fileId, frags};
 }
 
+std::vector<uint8_t> raw_id(const std::string& hex) {
+    std::vector<uint8_t> d(32, 0);
+    for (size_t i = 0; i < 32 && 2 * i + 1 < hex.size(); ++i) d[i] = static_cast<uint8_t>(std::stoi(hex.substr(2 * i, 2), nullptr, 16));
+    return d;
+}
+
 struct Node {
     int id;
     bool up = true;
-    std::map<std::string, std::map<int, dfs::Bytes>> fragments;  // data/node-<id>/<fileId>/fragments/<i>.frag
-    std::map<std::string, std::string> manifests;                // data/node-<id>/<fileId>/manifest.json
+    std::string root;                              // dataRoot = data/node-<id> (SN:20)
+    std::map<std::string, std::string> manifests;  // data/node-<id>/<fileId>/manifest.json
+
+    // Files.createDirectories + Files.write(<i>.frag) (SN:149, 166; 275, 285)
+    void saveFragment(const std::string& fileId, int index, const dfs::Bytes& b) {
+        const auto d = raw_id(fileId);
+        dfs_frag_ref ref{0, b.size(), 0, static_cast<uint32_t>(index)};
+        int32_t st = 0;
+        const int rc = dfs_store_write_fragments(nullptr, root.c_str(), d.data(), b.data(), &ref, 1, &st, 0);
+        if (rc != DFS_OK) throw std::runtime_error(std::string("Files.write: ") + dfs_strerror(rc));
+    }
+    // tryLoadFragmentLocal (SN:463-469): the bytes, or nullopt if absent
+    std::optional<dfs::Bytes> loadFragment(const std::string& fileId, int index) const {
+        std::error_code ec;
+        const fs::path p = fs::path(root) / fileId / "fragments" / (std::to_string(index) + ".frag");
+        if (!fs::exists(p, ec)) return std::nullopt;
+        const uint64_t sz = fs::file_size(p, ec);
+        if (ec) throw std::runtime_error("readAllBytes: " + ec.message());
+        dfs::Bytes b(sz);
+        const auto d = raw_id(fileId);
+        dfs_frag_ref ref{0, sz, 0, static_cast<uint32_t>(index)};
+        uint64_t len = 0;
+        int32_t st = 0;
+        const int rc = dfs_store_read_fragments(nullptr, root.c_str(), d.data(), b.data(), &ref, 1, &len, &st, 0);
+        if (st == DFS_E_MISSING) return std::nullopt;
+        if (rc != DFS_OK) throw std::runtime_error(std::string("readAllBytes: ") + dfs_strerror(rc));
+        b.resize(len);
+        return b;
+    }
 };
 
 struct Cluster {
     dfs::FragmentEngine eng;
     std::vector<Node> nodes;
-    Cluster() {
+    explicit Cluster(const std::string& data) {
         for (int i = 1; i <= TOTAL_NODES; ++i) {
             nodes.emplace_back();
             nodes.back().id = i;
+            nodes.back().root = data + "/node-" + std::to_string(i);
+            fs::create_directories(nodes.back().root);  // SN:24
         }
     }
     Node& node(int id) { return nodes[id - 1]; }
@@ -98,7 +142,7 @@ struct Cluster {
         std::vector<std::pair<int, std::pair<dfs::Bytes, std::string>>> dev;
         if (eng.receiveStoreBody(body, fileId, dev)) {  // device parse + decode + hash
             for (auto& kv : dev) {
-                n.fragments[fileId][kv.first] = kv.second.first;  // Files.write(<i>.frag), SN:284-285
+                n.saveFragment(fileId, kv.first, kv.second.first);  // Files.write(<i>.frag), SN:284-285
                 resp[kv.first] = kv.second.second;
             }
             return resp;
@@ -106,7 +150,7 @@ struct Cluster {
         auto parsed = parseJson(body);  // any other body form: the reference's parser
         auto got = eng.storeFragments(parsed.second);
         for (auto& kv : got) {
-            n.fragments[parsed.first][kv.first] = kv.second.first;  // Files.write(<i>.frag), SN:284-285
+            n.saveFragment(parsed.first, kv.first, kv.second.first);  // Files.write(<i>.frag), SN:284-285
             resp[kv.first] = kv.second.second;
         }
         return resp;
@@ -123,7 +167,7 @@ struct Cluster {
         for (const auto& f : up.second) {
             std::printf("[%d] Fragment %d: %zu bytes, hash=%s\n", u, f.index, f.data.size(), f.hash.c_str());
             if (f.index == my1 || f.index == my2) {
-                node(u).fragments[fileId][f.index] = f.data;
+                node(u).saveFragment(fileId, f.index, f.data);  // SN:165-166
                 std::printf("[%d] Saved fragment %d locally\n", u, f.index);
             }
         }
@@ -168,10 +212,9 @@ struct Cluster {
         std::vector<std::optional<dfs::Bytes>> frags(TOTAL_NODES);
         plan.clear();
         for (int i = 0; i < TOTAL_NODES; ++i) {
-            auto& local = node(r).fragments[fileId];
             std::string src = "missing";
-            if (local.count(i)) {
-                frags[i] = local[i];
+            if (auto local = node(r).loadFragment(fileId, i)) {  // SN:421
+                frags[i] = std::move(local);
                 src = "local";
             } else {
                 const int cand[2] = {i + 1, ((i - 1 + TOTAL_NODES) % TOTAL_NODES) + 1};  // SN:427-428
@@ -179,9 +222,9 @@ struct Cluster {
                     if (nd == r) continue;  // SN:433
                     Node& peer = node(nd);
                     if (!peer.up) continue;  // IOException swallowed, SN:439
-                    auto it = peer.fragments[fileId].find(i);
-                    if (it == peer.fragments[fileId].end()) continue;  // 404 -> null
-                    frags[i] = it->second;
+                    auto got = peer.loadFragment(fileId, i);  // getFragment, SN:471-483
+                    if (!got) continue;                        // 404 -> null
+                    frags[i] = std::move(got);
                     src = "node" + std::to_string(nd);
                     break;
                 }
@@ -199,8 +242,29 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "usage: %s <file>...\n", argv[0]);
         return 2;
     }
+    std::string data;
+    bool keep = false;
+    if (const char* d = std::getenv("DFS_SIM_DATA")) {
+        data = d;
+        keep = true;
+    } else {
+        char tmpl[] = "/tmp/dfs_sim_XXXXXX";
+        if (!mkdtemp(tmpl)) {
+            std::perror("mkdtemp");
+            return 3;
+        }
+        data = tmpl;
+    }
+    struct Cleanup {
+        std::string dir;
+        bool keep;
+        ~Cleanup() {
+            std::error_code ec;
+            if (!keep) fs::remove_all(dir, ec);
+        }
+    } cleanup{data, keep};
     try {
-        Cluster c;
+        Cluster c(data);
         std::vector<std::pair<std::string, dfs::Bytes>> files;
         std::vector<std::string> ids;
         for (int a = 1; a < argc; ++a) {
