@@ -481,17 +481,19 @@ def test_profiling_timings(engine):
         engine.set_profiling(False)
 
 
-def test_storage_node_sim_config1(golden):
+def test_storage_node_sim_config1(golden, tmp_path):
     """BASELINE config 1 replayed through the C++ host mirror: 5 nodes, upload
     examples/* at node 1, node 3 down, download at nodes 1, 2, 4, 5.  The
     fragment log lines must equal the golden ones and the
-    fetch plans the reference's."""
+    fetch plans the reference's; every node's data directory
+    holds exactly its pair as raw .frag files (SN:143-145, 163-166, 284-285)."""
     import subprocess
     from conftest import EXAMPLES, PKG
     names = [e["name"] for e in golden["examples"]]
     exe = os.path.join(PKG, "host", "storage_node_sim")
+    env = dict(os.environ, DFS_SIM_DATA=str(tmp_path / "data"))
     r = subprocess.run([exe] + [os.path.join(EXAMPLES, n) for n in names], capture_output=True, text=True,
-                       timeout=120)
+                       timeout=120, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     lines = r.stdout.splitlines()
     frag_lines = [l for l in lines if l.startswith("[1] Fragment ")]
@@ -505,6 +507,16 @@ def test_storage_node_sim_config1(golden):
                 me, e["name"], e["fileId"], ",".join(plans[str(me)]), e["size"])
             assert want in lines, want
     assert "[1] Download with nodes 2,3 down -> 500 Could not retrieve fragment 2" in lines
+    for e in golden["examples"]:
+        data = open(os.path.join(EXAMPLES, e["name"]), "rb").read()
+        spans = O.py_split(len(data), 5)
+        for k in range(5):
+            fdir = tmp_path / "data" / f"node-{k + 1}" / e["fileId"] / "fragments"
+            held = sorted(os.listdir(fdir))
+            assert held == sorted(f"{i}.frag" for i in O.py_node_fragments(k, 5))
+            for i in O.py_node_fragments(k, 5):
+                o, l = spans[i]
+                assert (fdir / f"{i}.frag").read_bytes() == data[o:o + l]
 
 
 def test_concurrent_handlers_share_one_ctx(engine):
