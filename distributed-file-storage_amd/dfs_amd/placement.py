@@ -86,6 +86,26 @@ def download_sources(n: int, world: int, me: int, offline: Iterable[int] = ()) -
 # ---------------------------------------------------------------------------
 # Exchanges (torch.distributed point-to-point; RCCL on GPU, gloo on CPU)
 # ---------------------------------------------------------------------------
+def file_owner(file_digest: torch.Tensor, world: int) -> torch.Tensor:
+    """Lookup rank of files after the upload: files are
+    sharded by index for hashing, but a later GET /download?fileId=<hex>
+    (SN:399-403) only knows the fileId, so the owner is the digest's first 8
+    bytes (big-endian, the first 16 hex chars) mod world.  file_digest:
+    (n, 32) uint8 raw digests on any device; returns (n,) int64 ranks, computed
+    where the digests live (no host round trip)."""
+    d = file_digest.reshape(-1, 32)[:, :8].to(torch.int64)
+    # prefix mod world, one byte at a time: (acc * 256 + byte) mod world
+    acc = torch.zeros(d.shape[0], dtype=torch.int64, device=d.device)
+    for j in range(8):
+        acc = (acc * 256 + d[:, j]) % world
+    return acc
+
+
+def file_owner_hex(file_id: str, world: int) -> int:
+    """file_owner for one lowercase-hex fileId (the HTTP side)."""
+    return int(file_id[:16], 16) % world
+
+
 def _all_sizes(local: Sequence[int], device) -> torch.Tensor:
     """[world, len(local)] int64 table of every rank's sizes."""
     world = dist.get_world_size()

@@ -119,3 +119,17 @@ def test_pure_maps():
         assert got == O.py_download_plan(me1, 5, O.py_node_fragments(me1 - 1, 5), down=[3])
     # two adjacent GPUs down: fragment between them is lost
     assert P.download_sources(5, 5, 0, offline=[2, 3])[3] is None
+
+
+def test_file_owner_digest_prefix():
+    """Owner of a fileId = first 8 digest bytes (big-endian) mod world, the
+    same from raw digests (device-side path) and from the hex string."""
+    import hashlib
+    import torch
+    from dfs_amd.placement import file_owner, file_owner_hex
+    ids = [hashlib.sha256(bytes([i]) * i).digest() for i in range(200)] + [b"\xff" * 32, b"\x00" * 32]
+    dig = torch.tensor([list(x) for x in ids], dtype=torch.uint8)
+    for world in (1, 2, 3, 5, 8):
+        got = file_owner(dig, world).tolist()
+        want = [int.from_bytes(x[:8], "big") % world for x in ids]
+        assert got == want == [file_owner_hex(x.hex(), world) for x in ids]
