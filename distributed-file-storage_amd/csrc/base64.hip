@@ -25,15 +25,6 @@ __device__ __forceinline__ uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32
     return __builtin_amdgcn_alignbyte(hi, lo, s);
 }
 
-// Four ASCII chars (first char in the low byte) of one 24-bit group.
-__device__ __forceinline__ uint32_t enc4(const uint8_t* __restrict__ lut, uint32_t v) {
-    const uint32_t c0 = lut[v >> 18];
-    const uint32_t c1 = lut[(v >> 12) & 63u];
-    const uint32_t c2 = lut[(v >> 6) & 63u];
-    const uint32_t c3 = lut[v & 63u];
-    return c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
-}
-
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // 64-entry alphabet as LE words (kAlphaWords) expanded to a 4,096-entry
@@ -79,10 +70,10 @@ __device__ __forceinline__ uint32_t grp(const uint32_t (&raw)[4]) {
 // One tile of full 12-byte groups whose source starts SA bytes past a dword
 // boundary.  tsrc (dword aligned, = first group - SA) and tdst are uniform;
 // every per-lane address is a constant 32-bit offset from them.
-template <int PER, int NT, bool PAIR, int SA>
+template <int SA>
 __device__ __forceinline__ void enc_tile(const uint32_t* __restrict__ tsrc, uint8_t* __restrict__ tdst,
-                                         int64_t left, const uint8_t* __restrict__ lut,
-                                         const uint16_t* __restrict__ pair) {
+                                         int64_t left, const uint16_t* __restrict__ pair) {
+    constexpr int PER = kEncPer;
     uint32_t raw[PER][4];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -91,16 +82,12 @@ __device__ __forceinline__ void enc_tile(const uint32_t* __restrict__ tsrc, uint
         if (static_cast<int64_t>(lg) < left) {
             const uint32_t* w = tsrc + 3u * lg;
             if (SA) {
-                u32x4 v;
-                if (NT & 2) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
-                else v = *reinterpret_cast<const u32x4*>(w);
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
                 raw[i][0] = v.x; raw[i][1] = v.y; raw[i][2] = v.z; raw[i][3] = v.w;
-            } else if (NT & 2) {
+            } else {
                 raw[i][0] = __builtin_nontemporal_load(w);
                 raw[i][1] = __builtin_nontemporal_load(w + 1);
                 raw[i][2] = __builtin_nontemporal_load(w + 2);
-            } else {
-                raw[i][0] = w[0]; raw[i][1] = w[1]; raw[i][2] = w[2];
             }
         }
     }
@@ -109,26 +96,16 @@ __device__ __forceinline__ void enc_tile(const uint32_t* __restrict__ tsrc, uint
         const uint32_t lg = threadIdx.x + static_cast<uint32_t>(i) * kStreamBlock;
         if (static_cast<int64_t>(lg) < left) {
             uint32_t g[4] = {grp<SA>(raw[i]), grp<SA + 3>(raw[i]), grp<SA + 6>(raw[i]), grp<SA + 9>(raw[i])};
-            u32x4 o;
-            if (PAIR) {
-                o = u32x4{enc4_pair(pair, g[0]), enc4_pair(pair, g[1]), enc4_pair(pair, g[2]), enc4_pair(pair, g[3])};
-            } else {
-                o = u32x4{enc4(lut, g[0]), enc4(lut, g[1]), enc4(lut, g[2]), enc4(lut, g[3])};
-            }
-            u32x4* d = reinterpret_cast<u32x4*>(tdst + 16u * lg);
-            if (NT & 1) __builtin_nontemporal_store(o, d);
-            else *d = o;
+            const u32x4 o{enc4_pair(pair, g[0]), enc4_pair(pair, g[1]), enc4_pair(pair, g[2]), enc4_pair(pair, g[3])};
+            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(tdst + 16u * lg));
         }
     }
 }
 
-// PER groups per thread per tile (tile = PER*256 groups); NT bit 0 =
-// non-temporal (streaming) stores, bit 1 = non-temporal loads: this pass
-// never re-reads the Base64 it writes, and its input only via the SHA kernel
-// beside it (which is why loads stay temporal by default).  PAIR selects the
-// 12-bit pair table (2 LDS reads + 5 VALU per group) over the 6-bit
-// alphabet (4 LDS reads + ~10 VALU per group).
-template <int PER, int NT, bool PAIR>
+// kEncPer groups per thread per tile (tile = 4 x 256 groups); loads and
+// stores are non-temporal (streaming): this pass touches every byte once.
+// The 12-bit pair table costs 2 LDS reads + 5 VALU per group (a 6-bit
+// alphabet would be 4 LDS reads + ~10 VALU).
 __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t* __restrict__ base,
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
@@ -141,15 +118,9 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
         case 2: __builtin_amdgcn_s_setprio(2); break;
         default: __builtin_amdgcn_s_setprio(3); break;
     }
-    __shared__ uint32_t lut_words[PAIR ? 2048 : 16];
-    if (PAIR) {
-        build_pair_lut(reinterpret_cast<uint16_t*>(lut_words));
-    } else if (threadIdx.x < 16) {
-        lut_words[threadIdx.x] = kAlphaWords[threadIdx.x];
-    }
+    __shared__ uint16_t pair[4096];
+    build_pair_lut(pair);
     __syncthreads();
-    const uint8_t* lut = reinterpret_cast<const uint8_t*>(lut_words);
-    const uint16_t* pair = reinterpret_cast<const uint16_t*>(lut_words);
 
     uint64_t t0, t1;
     tile_range(ntiles, t0, t1);
@@ -163,18 +134,18 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
         const uint8_t* __restrict__ src = base + jobs[j].src_off;
         uint8_t* __restrict__ dst = reinterpret_cast<uint8_t*>(out) + jobs[j].dst_off;
         const uint32_t sa = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src)) & 3u;
-        const uint64_t tg = (t - jobs[j].tile_start) * (PER * kStreamBlock);  // first group of the tile
+        const uint64_t tg = (t - jobs[j].tile_start) * (kEncPer * kStreamBlock);  // first group of the tile
         const int64_t left = static_cast<int64_t>(nfg) - static_cast<int64_t>(tg);
         const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(src + 12 * tg - sa);
         uint8_t* tdst = dst + 16 * tg;
         switch (sa) {  // wave-uniform
-            case 0: enc_tile<PER, NT, PAIR, 0>(tsrc, tdst, left, lut, pair); break;
-            case 1: enc_tile<PER, NT, PAIR, 1>(tsrc, tdst, left, lut, pair); break;
-            case 2: enc_tile<PER, NT, PAIR, 2>(tsrc, tdst, left, lut, pair); break;
-            default: enc_tile<PER, NT, PAIR, 3>(tsrc, tdst, left, lut, pair); break;
+            case 0: enc_tile<0>(tsrc, tdst, left, pair); break;
+            case 1: enc_tile<1>(tsrc, tdst, left, pair); break;
+            case 2: enc_tile<2>(tsrc, tdst, left, pair); break;
+            default: enc_tile<3>(tsrc, tdst, left, pair); break;
         }
         // Last partial group: full triples then "==" / "=" padding (RFC 4648 §4).
-        if (rem && left >= 0 && left < PER * kStreamBlock && threadIdx.x == static_cast<uint32_t>(left) % kStreamBlock) {
+        if (rem && left >= 0 && left < kEncPer * kStreamBlock && threadIdx.x == static_cast<uint32_t>(left) % kStreamBlock) {
             uint32_t* o = reinterpret_cast<uint32_t*>(dst + 16 * nfg);
             const uint8_t* s = src + 12 * nfg;
             for (uint32_t k = 0; k < rem; k += 3) {
@@ -182,7 +153,7 @@ __global__ __launch_bounds__(kStreamBlock) void b64_encode_kernel(const uint8_t*
                 uint32_t v = static_cast<uint32_t>(s[k]) << 16;
                 if (n > 1) v |= static_cast<uint32_t>(s[k + 1]) << 8;
                 if (n > 2) v |= s[k + 2];
-                uint32_t wv = PAIR ? enc4_pair(pair, v) : enc4(lut, v);
+                uint32_t wv = enc4_pair(pair, v);
                 if (n == 1) wv = (wv & 0x0000ffffu) | 0x3d3d0000u;  // "xx=="
                 else if (n == 2) wv = (wv & 0x00ffffffu) | 0x3d000000u;  // "xxx="
                 o[k / 3] = wv;
@@ -294,23 +265,22 @@ __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const 
     }
 }
 
-// One tile = GPL x 256 4-unit groups (GPL = 4: 16 KiB of chars -> 12 KiB of
+// One tile = GPL x 256 4-unit groups (GPL = 8: 32 KiB of chars -> 24 KiB of
 // output).  Phase 1: lane l loads groups 256i + l (i < GPL) with one dwordx4
-// each (a wave reads 1 KiB contiguous per instruction, all four loads in
+// each (a wave reads 1 KiB contiguous per instruction, all eight loads in
 // flight), decodes them through the LDS alphabet and parks the 12 bytes of
 // each at LDS offset 12 * group.  Phase 2: lane l cuts 16-byte output chunks
 // 256i + l (i < 3) out of the decoded stream at byte offset e and writes
 // each with one dwordx4 store at a 16-byte aligned address (a wave writes
 // 1 KiB contiguous per instruction).  Head, tail and final unit: dec_tail,
-// on wave 0 of the message's last tile.  NT bit 0 = non-temporal stores,
-// bit 1 = non-temporal loads.
-template <int NT, int GPL>
+// on wave 0 of the message's last tile.  Loads and stores are non-temporal.
 __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
                                                                   uint8_t* __restrict__ out,
                                                                   int32_t* __restrict__ status,
                                                                   uint64_t* __restrict__ out_len) {
+    constexpr int GPL = kDecGpl;
     constexpr uint32_t kGroups = GPL * kStreamBlock;  // 4-unit groups per tile
     constexpr uint32_t kChunks = 3 * GPL * 64;        // 16-byte output chunks per tile (12 kGroups / 16)
     __shared__ uint8_t lut[256];
@@ -339,11 +309,9 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
             raw[i][0] = raw[i][1] = raw[i][2] = raw[i][3] = raw[i][4] = 0u;
             if (g < G.ng) {
                 const uint32_t* w = w0 + 4 * g;
-                u32x4 v;
-                if (NT & 2) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
-                else v = *reinterpret_cast<const u32x4*>(w);
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(w));
                 raw[i][0] = v.x; raw[i][1] = v.y; raw[i][2] = v.z; raw[i][3] = v.w;
-                if (sa) raw[i][4] = (NT & 2) ? __builtin_nontemporal_load(w + 4) : w[4];
+                if (sa) raw[i][4] = __builtin_nontemporal_load(w + 4);
             }
         }
         uint32_t bad = 0;
@@ -378,9 +346,7 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
                 const uint32_t n4 = G.e ? stream[4 * m + 4] : 0u;
                 const u32x4 o = u32x4{align_bytes(a.y, a.x, G.e), align_bytes(a.z, a.y, G.e),
                                       align_bytes(a.w, a.z, G.e), align_bytes(n4, a.w, G.e)};
-                u32x4* d = reinterpret_cast<u32x4*>(dst + G.h + 16 * (c0 + m));
-                if (NT & 1) __builtin_nontemporal_store(o, d);
-                else *d = o;
+                __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(dst + G.h + 16 * (c0 + m)));
             }
         }
         if (threadIdx.x < 64 && t + 1 == jobs[j + 1].tile_start)  // wave 0 of the message's last tile
@@ -392,42 +358,18 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
 }  // namespace
 
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, char* out,
-                             uint32_t wgs_per_cu, hipStream_t s, int per, int nt, bool pair, uint32_t prio) {
+                             uint32_t wgs_per_cu, hipStream_t s, uint32_t prio) {
     if (ntiles == 0) return hipSuccess;
-    const dim3 g(stream_grid(ntiles, wgs_per_cu)), b(kStreamBlock);
-#define DFS_ENC(P, N, L) hipLaunchKernelGGL((b64_encode_kernel<P, N, L>), g, b, 0, s, base, jobs, njobs, ntiles, out, prio)
-#define DFS_ENC_NT(P, L)                   \
-    switch (nt & 3) {                      \
-        case 0: DFS_ENC(P, 0, L); break;   \
-        case 1: DFS_ENC(P, 1, L); break;   \
-        case 2: DFS_ENC(P, 2, L); break;   \
-        default: DFS_ENC(P, 3, L); break;  \
-    }
-    if (per == 8) {
-        if (pair) { DFS_ENC_NT(8, true) } else { DFS_ENC_NT(8, false) }
-    } else {
-        if (pair) { DFS_ENC_NT(4, true) } else { DFS_ENC_NT(4, false) }
-    }
-#undef DFS_ENC_NT
-#undef DFS_ENC
+    hipLaunchKernelGGL(b64_encode_kernel, dim3(stream_grid(ntiles, wgs_per_cu)), dim3(kStreamBlock), 0, s, base, jobs,
+                       njobs, ntiles, out, prio);
     return hipGetLastError();
 }
 
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                             int32_t* status, uint64_t* out_len, hipStream_t s, int nt, int gpl) {
+                             int32_t* status, uint64_t* out_len, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
-    const dim3 g(stream_grid(ntiles)), b(kStreamBlock);
-#define DFS_DEC(N, G) hipLaunchKernelGGL((b64_decode_kernel<N, G>), g, b, 0, s, in, jobs, njobs, ntiles, out, status, out_len)
-#define DFS_DEC_NT(G)                  \
-    switch (nt & 3) {                  \
-        case 0: DFS_DEC(0, G); break;  \
-        case 1: DFS_DEC(1, G); break;  \
-        case 2: DFS_DEC(2, G); break;  \
-        default: DFS_DEC(3, G); break; \
-    }
-    if (gpl == 2) { DFS_DEC_NT(2) } else if (gpl == 4) { DFS_DEC_NT(4) } else { DFS_DEC_NT(8) }
-#undef DFS_DEC_NT
-#undef DFS_DEC
+    hipLaunchKernelGGL(b64_decode_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, in, jobs, njobs, ntiles,
+                       out, status, out_len);
     return hipGetLastError();
 }
 

@@ -66,25 +66,27 @@ struct dfs_ctx {
     int sha_wps_beside = 3;      // ... when the Base64 kernel runs beside it (4 x 116 VGPRs leave no room)
     int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels (DFS_UPLOAD_MODE)
     int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
-    int b64_per = 4;             // encode groups per thread per tile (DFS_B64_PER: 4 or 8)
-    int b64_nt = 3;              // non-temporal encode: bit 0 stores, bit 1 loads (DFS_B64_NT)
-    int dec_nt = 3;              // non-temporal decode: bit 0 stores, bit 1 loads (DFS_DEC_NT)
-    int gather_per = 4;          // gather: 16-byte chunks per thread per tile, 4 or 8 (DFS_GATHER_PER)
-    int dec_gpl = 8;             // decode: 4-unit groups per thread per tile, 2, 4 or 8 (DFS_DEC_GPL)
-    bool b64_pair = true;        // 12-bit pair table (DFS_B64_LUT=12) vs 6-bit alphabet (=6)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
+    hipEvent_t fork = nullptr, join = nullptr;  // SHA || Base64 on two streams
+    // The scratch buffers (buf[]) are reused by the next call.  An async call
+    // leaves them in use on its stream: a call on another stream (after
+    // dfs_set_stream) first waits for scratch_ev (recorded after the last
+    // launch that used them) so it cannot overwrite descriptors in flight.
+    hipEvent_t scratch_ev = nullptr;
+    hipStream_t scratch_stream = nullptr;
     DevBuf buf[B_COUNT];
     dfs::StoreStaging* store = nullptr;  // pinned staging ring of the fragment store
     std::mutex mu;
+    std::mutex store_mu;         // the fragment store's staging ring (fragstore.cpp)
     hipStream_t stream() const { return user ? user : own; }
 };
 
 namespace dfs {
 hipStream_t ctx_stream(dfs_ctx* c) { return c->stream(); }
 int ctx_device(dfs_ctx* c) { return c->device; }
-std::mutex& ctx_mutex(dfs_ctx* c) { return c->mu; }
+std::mutex& ctx_store_mutex(dfs_ctx* c) { return c->store_mu; }
 StoreStaging*& ctx_store(dfs_ctx* c) { return c->store; }
 }  // namespace dfs
 
@@ -99,7 +101,6 @@ struct dfs_upload_plan {
     StreamJob* d_enc = nullptr;
     uint32_t n_enc = 0;
     uint64_t enc_tiles = 0;
-    int enc_per = 4;  // groups per thread the encode tiles were built for
     std::vector<uint64_t> b64_off;
     uint64_t b64_total = 0;
 };
@@ -215,6 +216,18 @@ struct Timer {
     }
 };
 
+// Scope of one call's use of the ctx scratch on stream s (see dfs_ctx).
+struct Scratch {
+    dfs_ctx* c;
+    hipStream_t s;
+    Scratch(dfs_ctx* ctx, hipStream_t st) : c(ctx), s(st) {
+        if (c->scratch_stream && c->scratch_stream != s) (void)hipStreamWaitEvent(s, c->scratch_ev, 0);
+    }
+    ~Scratch() {
+        if (hipEventRecord(c->scratch_ev, s) == hipSuccess) c->scratch_stream = s;
+    }
+};
+
 int put(dfs_ctx* c, int id, const void* src, size_t n, hipStream_t s) {
     HIPC(c->buf[id].ensure(n));
     if (n) HIPC(hipMemcpyAsync(c->buf[id].p, src, n, hipMemcpyHostToDevice, s));
@@ -264,17 +277,14 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = c->sha_wps_beside = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_UPLOAD_MODE")) c->upload_mode = std::strcmp(w, "fused") == 0 ? 0 : 1;
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
-    if (const char* w = std::getenv("DFS_B64_PER")) c->b64_per = std::atoi(w) == 8 ? 8 : 4;
-    if (const char* w = std::getenv("DFS_B64_NT")) c->b64_nt = std::atoi(w) & 3;
-    if (const char* w = std::getenv("DFS_DEC_NT")) c->dec_nt = std::atoi(w) & 3;
-    if (const char* w = std::getenv("DFS_GATHER_PER")) c->gather_per = std::atoi(w) == 8 ? 8 : 4;
-    if (const char* w = std::getenv("DFS_DEC_GPL")) c->dec_gpl = std::atoi(w) == 2 ? 2 : std::atoi(w) == 4 ? 4 : 8;
-    if (const char* w = std::getenv("DFS_B64_LUT")) c->b64_pair = std::atoi(w) != 6;
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
     for (int i = 0; e == hipSuccess && i < 2 * DFS_T_COUNT; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         dfs_close(c);
         return hip_fail(e, "dfs_open");
@@ -291,6 +301,8 @@ int dfs_close(dfs_ctx* c) {
     for (auto& b : c->buf) b.release();
     dfs::store_staging_free(c->store);
     for (auto& ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : {c->fork, c->join, c->scratch_ev})
         if (ev) (void)hipEventDestroy(ev);
     if (c->own) (void)hipStreamDestroy(c->own);
     if (c->aux) (void)hipStreamDestroy(c->aux);
@@ -355,6 +367,7 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
     if (!n) return DFS_OK;
     const bool dev = flags & DFS_DEVICE_PTRS;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     std::vector<ShaDesc> d(n);
     uint64_t end = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -377,7 +390,7 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
-                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -398,6 +411,7 @@ int dfs_sha256_update_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* par
     if (!n) return DFS_OK;
     const bool dev = flags & DFS_DEVICE_PTRS;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     std::vector<ShaDesc> d(n);
     uint64_t end = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -426,7 +440,7 @@ int dfs_sha256_update_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* par
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(dfs::launch_sha256(d_base, c->buf[B_DESC].as<ShaDesc>(), n, n, prio, d_dig, d_dig,
-                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, d_state));
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s, d_state));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -460,6 +474,7 @@ int dfs_receive_fragments_batch(dfs_ctx* c, const char* in, const dfs_span* msgs
         std::lock_guard<std::mutex> lk(c->mu);
         if (int e = enter(c)) return e;
         hipStream_t s = c->stream();
+        Scratch scratch(c, s);
         std::vector<ShaDesc> d(ok.size());
         for (size_t k = 0; k < ok.size(); ++k) d[k] = msg(ok[k].off, ok[k].len, k);
         const uint32_t prio = sort_lanes(d);
@@ -468,8 +483,7 @@ int dfs_receive_fragments_batch(dfs_ctx* c, const char* in, const dfs_span* msgs
         HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
         HIPC(dfs::launch_sha256(out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(d.size()),
                                 static_cast<uint32_t>(d.size()), prio, c->buf[B_DIG1].as<uint8_t>(),
-                                c->buf[B_DIG1].as<uint8_t>(), c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr,
-                                s));
+                                c->buf[B_DIG1].as<uint8_t>(), c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s));
         HIPC(hipMemcpyAsync(dig.data(), c->buf[B_DIG1].p, dig.size(), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
     } else {
@@ -488,6 +502,7 @@ int dfs_sha256_update_parts(dfs_ctx* c, const uint8_t* base, const dfs_part* par
     Timer tm(c);
     if (!n) return DFS_OK;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     std::vector<ShaDesc> d(n);
     uint64_t end = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -506,7 +521,7 @@ int dfs_sha256_update_parts(dfs_ctx* c, const uint8_t* base, const dfs_part* par
     tm.begin(DFS_T_SHA, s);
     // digests indexed by slot: split = UINT32_MAX keeps every slot in out0
     HIPC(dfs::launch_sha256(base, c->buf[B_DESC].as<ShaDesc>(), n, UINT32_MAX, prio, digests, digests,
-                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s, state));
+                            c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s, state));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     return DFS_OK;
@@ -521,6 +536,7 @@ int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, 
     Timer tm(c);
     const bool dev = flags & DFS_DEVICE_PTRS;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     uint64_t total = 0, end = 0;
     std::vector<StreamJob> jobs;
     std::vector<uint64_t> items;
@@ -541,7 +557,7 @@ int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, 
     out_off[n] = total;
     if (total > out_cap || (total && !out) || (end && !base)) return DFS_E_ARG;
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->b64_per) * dfs::kStreamBlock);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
     const uint8_t* d_base = base;
     char* d_out = out;
     if (!dev) {
@@ -555,8 +571,7 @@ int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, 
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64ENC, s);
-    HIPC(dfs::launch_b64_encode(d_base, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s, c->b64_per,
-                                c->b64_nt, c->b64_pair));
+    HIPC(dfs::launch_b64_encode(d_base, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s));
     tm.end(DFS_T_B64ENC, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -576,6 +591,7 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
     if (!n) return DFS_OK;
     const bool dev = flags & DFS_DEVICE_PTRS;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     uint64_t in_end = 0, out_end = 0;
     for (uint32_t i = 0; i < n; ++i) {
         in_end = std::max(in_end, msgs[i].off + msgs[i].len);
@@ -601,7 +617,7 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
         j.id = i;
         items[i] = dec_items(msgs[i].len, reinterpret_cast<uintptr_t>(d_out + out_off[i]));
     }
-    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->dec_gpl) * dfs::kStreamBlock);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * n));
     HIPC(c->buf[B_OUTLEN].ensure(8ull * n));
@@ -609,8 +625,7 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64DEC, s);
     HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), n, ntiles, d_out,
-                                c->buf[B_STATUS].as<int32_t>(), c->buf[B_OUTLEN].as<uint64_t>(), s,
-                                c->dec_nt, c->dec_gpl));
+                                c->buf[B_STATUS].as<int32_t>(), c->buf[B_OUTLEN].as<uint64_t>(), s));
     tm.end(DFS_T_B64DEC, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(n);
@@ -713,8 +728,7 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     p->n_all = static_cast<uint32_t>(all.size());
     p->n_frag_only = static_cast<uint32_t>(frag.size());
     p->n_enc = static_cast<uint32_t>(enc.size());
-    p->enc_per = c->b64_per;
-    p->enc_tiles = finish_jobs(enc, items, static_cast<uint64_t>(p->enc_per) * dfs::kStreamBlock);
+    p->enc_tiles = finish_jobs(enc, items, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
     hipError_t e = hipMalloc(&p->d_queue, dfs::kShaQueueBytes);
     if (e == hipSuccess) e = hipMalloc(&p->d_all, std::max<size_t>(all.size(), 1) * sizeof(ShaDesc));
     if (e == hipSuccess) e = hipMalloc(&p->d_frag, std::max<size_t>(frag.size(), 1) * sizeof(ShaDesc));
@@ -761,68 +775,48 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     if (!d_frd || (do_fileid && !d_fd) || (do_b64 && !d_b64)) return DFS_E_ARG;
     if (do_b64 && (reinterpret_cast<uintptr_t>(d_b64) & 3u)) return DFS_E_ARG;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     if (flags & DFS_B64_ONLY) {  // the HBM-bound encode pass alone
         if (!do_b64) return DFS_OK;
         Timer tb(c);
         tb.begin(DFS_T_TOTAL, s);
         tb.begin(DFS_T_B64ENC, s);
-        HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64, 8u, s, p->enc_per,
-                                    c->b64_nt, c->b64_pair, c->b64_prio));
+        HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64, 8u, s, c->b64_prio));
         tb.end(DFS_T_B64ENC, s);
         tb.end(DFS_T_TOTAL, s);
         return DFS_OK;
     }
     hipStream_t sb = serial ? s : c->aux;
     Timer tm(c);
-    // Experiment hook: DFS_SHA_CENSUS=<path> dumps {hw_id, xcc_id, t0, t1} per
-    // SHA work item (s_memrealtime, 100 MHz) after the call.
-    const char* census_path = std::getenv("DFS_SHA_CENSUS");
-    uint32_t* census = nullptr;
-    const uint32_t n_items = ((do_fileid ? p->n_all : p->n_frag_only) + 63u) / 64u;
-    if (census_path) {
-        HIPC(c->buf[B_OUTLEN].ensure(16ull * n_items));
-        census = c->buf[B_OUTLEN].as<uint32_t>();
-        HIPC(hipMemsetAsync(census, 0, 16ull * n_items, s));
-    }
     const bool two = do_b64 && !fused;  // separate Base64 encode kernel
     const int wps = two && !serial ? c->sha_wps_beside : c->sha_wps;
     tm.begin(DFS_T_TOTAL, s);
     if (two && !serial) {  // fork: Base64 on the aux stream beside SHA
-        HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER], s));
-        HIPC(hipStreamWaitEvent(sb, c->ev[2 * DFS_T_GATHER], 0));
+        HIPC(hipEventRecord(c->fork, s));
+        HIPC(hipStreamWaitEvent(sb, c->fork, 0));
     }
     // Fused: the fragment lanes write the Base64 too (kShaB64, sha256.hip).
     char* fb64 = fused ? d_b64 : nullptr;
     tm.begin(DFS_T_SHA, s);
     if (do_fileid) {
         HIPC(dfs::launch_sha256(d_files, p->d_all, p->n_all, p->nfiles, p->prio_all, d_fd, d_frd, p->d_queue,
-                                wps, census, s, nullptr, fb64));
+                                wps, s, nullptr, fb64));
     } else {
         HIPC(dfs::launch_sha256(d_files, p->d_frag, p->n_frag_only, p->nfiles, p->prio_frag, d_fd, d_frd,
-                                p->d_queue, wps, census, s, nullptr, fb64));
+                                p->d_queue, wps, s, nullptr, fb64));
     }
     tm.end(DFS_T_SHA, s);
     if (two) {
         tm.begin(DFS_T_B64ENC, sb);
         HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64,
-                                    serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb, p->enc_per, c->b64_nt,
-                                    c->b64_pair, c->b64_prio));
+                                    serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb, c->b64_prio));
         tm.end(DFS_T_B64ENC, sb);
         if (!serial) {  // join
-            HIPC(hipEventRecord(c->ev[2 * DFS_T_GATHER + 1], sb));
-            HIPC(hipStreamWaitEvent(s, c->ev[2 * DFS_T_GATHER + 1], 0));
+            HIPC(hipEventRecord(c->join, sb));
+            HIPC(hipStreamWaitEvent(s, c->join, 0));
         }
     }
     tm.end(DFS_T_TOTAL, s);
-    if (census_path) {
-        std::vector<uint32_t> h(4ull * n_items);
-        HIPC(hipMemcpyAsync(h.data(), census, h.size() * 4, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
-        if (FILE* fp = std::fopen(census_path, "wb")) {
-            std::fwrite(h.data(), 4, h.size(), fp);
-            std::fclose(fp);
-        }
-    }
     return DFS_OK;
 }
 }  // namespace
@@ -853,6 +847,7 @@ int dfs_upload_batch(dfs_ctx* c, const uint8_t* files, const dfs_span* spans, ui
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = enter(c)) return rc;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     const bool dev = flags & DFS_DEVICE_PTRS;
     uint64_t end = 0;
     for (uint32_t f = 0; f < nfiles; ++f) end = std::max(end, spans[f].off + spans[f].len);
@@ -895,6 +890,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     if (!nfiles) return DFS_OK;
     const bool dev = flags & DFS_DEVICE_PTRS;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
     std::vector<uint64_t> flen(nfiles, 0);
     uint64_t out_end = 0, stage = 0;
@@ -947,7 +943,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
         sha.push_back(msg(file_off[f], flen[f], f));  // SN:454
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->gather_per) * dfs::kStreamBlock);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kGatherPer) * dfs::kStreamBlock);
     const uint32_t prio = sort_lanes(sha);
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
@@ -955,12 +951,12 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_GATHER, s);
-    HIPC(dfs::launch_gather(c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s, c->gather_per));
+    HIPC(dfs::launch_gather(c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s));
     tm.end(DFS_T_GATHER, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
-                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, nullptr, s));
+                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<uint8_t> dig(32ull * nfiles);
@@ -988,6 +984,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     if (!nfiles) return DFS_OK;
     const bool dev = flags & DFS_DEVICE_PTRS;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
     uint64_t in_end = 0, out_end = 0;
     for (uint32_t f = 0; f < nfiles; ++f) {
@@ -1032,7 +1029,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         sha.push_back(msg(file_off[f], file_len[f], nf + f));
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->dec_gpl) * dfs::kStreamBlock);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
     const uint32_t prio = sort_lanes(sha);  // one message per lane, persistent sha256_lanes
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
@@ -1043,13 +1040,13 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     tm.begin(DFS_T_TOTAL, s);
     tm.begin(DFS_T_B64DEC, s);
     HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out,
-                                c->buf[B_STATUS].as<int32_t>(), nullptr, s, c->dec_nt, c->dec_gpl));
+                                c->buf[B_STATUS].as<int32_t>(), nullptr, s));
     tm.end(DFS_T_B64DEC, s);
     tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
                             static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(),
-                            c->sha_wps, nullptr, s));
+                            c->sha_wps, s));
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(nf);
@@ -1100,6 +1097,7 @@ int dfs_synth_fill_at(dfs_ctx* c, uint8_t* d_dst, const dfs_span* files, uint32_
     if (int rc = enter(c)) return rc;
     if (!nfiles) return DFS_OK;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     std::vector<StreamJob> jobs;
     std::vector<uint64_t> items;
     for (uint32_t f = 0; f < nfiles; ++f) {
@@ -1180,6 +1178,7 @@ int dfs_store_bodies_build(dfs_ctx* c, const uint8_t* files, const dfs_span* fil
     if (!nfiles) return DFS_OK;
     if ((end && !files) || !file_digest) return DFS_E_ARG;
     hipStream_t s = c->stream();
+    Scratch scratch(c, s);
     const uint8_t* d_files = files;
     const uint8_t* d_dig = file_digest;
     char* d_out = bodies;
@@ -1194,15 +1193,14 @@ int dfs_store_bodies_build(dfs_ctx* c, const uint8_t* files, const dfs_span* fil
         return DFS_E_ARG;
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(c->b64_per) * dfs::kStreamBlock);
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, desc.data(), desc.size() * sizeof(dfs::StoreBody), s)) return rc;
     tm.begin(DFS_T_TOTAL, s);
     HIPC(dfs::launch_store_body_frame(c->buf[B_DESC].as<dfs::StoreBody>(), static_cast<uint32_t>(desc.size()), d_dig,
                                       d_out, s));
     tm.begin(DFS_T_B64ENC, s);
-    HIPC(dfs::launch_b64_encode(d_files, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s, c->b64_per,
-                                c->b64_nt, c->b64_pair, 0u));
+    HIPC(dfs::launch_b64_encode(d_files, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, 8u, s, 0u));
     tm.end(DFS_T_B64ENC, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
@@ -1235,6 +1233,7 @@ int dfs_store_bodies_receive(dfs_ctx* c, const char* bodies, const dfs_span* bod
         std::lock_guard<std::mutex> lk(c->mu);
         if (int rc = enter(c)) return rc;
         hipStream_t s = c->stream();
+        Scratch scratch(c, s);
         const char* d_in = bodies;
         if (!dev) {
             if (int rc = put(c, B_DATA_IN, bodies, end, s)) return rc;

@@ -47,7 +47,9 @@ struct StreamJob {
 constexpr int kShaBlock = 256;       // threads per SHA workgroup (4 waves)
 constexpr size_t kShaQueueBytes = 4 * (64 + 8192);  // SHA queue words + per-SIMD tokens
 constexpr int kStreamBlock = 256;    // threads per stream workgroup
-constexpr int kEncGroupsPerTile = 1024;  // 12-byte groups (4 per thread)
+constexpr int kEncPer = 4;           // encode: 12-byte groups per thread per tile
+constexpr int kDecGpl = 8;           // decode: 4-unit groups per thread per tile
+constexpr int kGatherPer = 4;        // gather: 16-byte chunks per thread per tile
 // Base64 decode geometry of one message of L chars decoding to dst (shared
 // by the host's tile count and b64_decode_kernel).  q = L/4 full units, r =
 // L%4; the final unit (padded, or the r trailing chars) is decoded by the
@@ -77,12 +79,6 @@ __host__ __device__ inline DecGeom dec_geom(uint64_t L, uintptr_t dst) {
     g.ng = g.body_units > g.u_first ? (g.body_units - g.u_first) / 4 : 0;
     g.nchunks = 12 * g.ng > g.e ? (12 * g.ng - g.e) / 16 : 0;
     return g;
-}
-
-// Tiles per job.
-inline uint64_t enc_tiles(uint64_t len) {
-    uint64_t groups = (len + 11) / 12;
-    return (groups + kEncGroupsPerTile - 1) / kEncGroupsPerTile;
 }
 
 // One storeFragments request body (buildFragmentsJson, SN:629-642) carrying
@@ -116,22 +112,17 @@ struct BodyParse {
 // on each of the 1024 SIMDs (fewer for small batches).
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
-                         int waves_per_simd, uint32_t* census, hipStream_t s, uint32_t* state = nullptr,
-                         char* b64 = nullptr);
-// Tiles hold per*256 groups (per = 4 or 8, must match the tile count the jobs
-// were built with); nt bit 0 = non-temporal stores, bit 1 = non-temporal loads;
-// pair = 12-bit character-pair LDS table (else the 6-bit alphabet).
+                         int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr);
+// Tiles hold kEncPer*256 12-byte groups (the job table's tile_start must be
+// built with that tile size); prio = s_setprio of the encode waves.
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             char* out, uint32_t wgs_per_cu, hipStream_t s, int per = 4, int nt = 0,
-                             bool pair = true, uint32_t prio = 3);
+                             char* out, uint32_t wgs_per_cu, hipStream_t s, uint32_t prio = 3);
 // Decode: chars of job j at in + src_off decode to out + dst_off.
 // status[id] |= 1 on an IllegalArgumentException case; out_len[id] = bytes.
 // If job.expect != 0 it is the expected decoded length + 1 (download path):
-// a different length sets status bit 2.  nt bit 0 = non-temporal stores,
-// bit 1 = non-temporal loads.
+// a different length sets status bit 2.  Tiles hold kDecGpl*256 4-unit groups.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, int nt = 3,
-                             int gpl = 8);  // gpl: 4-unit groups per thread per tile (2, 4 or 8)
+                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s);
 // Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
 hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
                                    hipStream_t s);
@@ -140,14 +131,10 @@ hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const ui
 hipError_t launch_store_body_parse(const char* in, const uint64_t* spans, uint32_t n, BodyParse* out,
                                    char* file_ids, hipStream_t s);
 // Gather: job.src_off is an absolute device address of the fragment; tiles
-// of per x 256 16-byte chunks (per = 4 or 8).
-hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                         hipStream_t s, int per = 4);
+// of kGatherPer x 256 16-byte chunks.
+hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
                         hipStream_t s, uint64_t file_off);
-// Compare n digests a[i] vs b[i] (32 B each); status[i*stride] = code if different.
-hipError_t launch_digest_compare(const uint8_t* a, const uint8_t* b, uint32_t n, int32_t code,
-                                 int32_t* status, uint32_t status_div, hipStream_t s);
 
 // ctx internals for the on-disk fragment store (fragstore.cpp).  The store's
 // pinned staging ring lives in the ctx and is freed by dfs_close.
@@ -155,7 +142,7 @@ struct StoreStaging;
 void store_staging_free(StoreStaging* s);
 hipStream_t ctx_stream(dfs_ctx* c);
 int ctx_device(dfs_ctx* c);
-std::mutex& ctx_mutex(dfs_ctx* c);
+std::mutex& ctx_store_mutex(dfs_ctx* c);  // guards the staging ring only
 StoreStaging*& ctx_store(dfs_ctx* c);
 
 }  // namespace dfs

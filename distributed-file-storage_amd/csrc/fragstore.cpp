@@ -13,7 +13,14 @@
 // while a thread pool writes slot b to disk, the DMA engine fills slot b+1
 // from HBM (upload); on download the pool reads slot b+1 from disk while
 // slot b is copied into HBM.  Fragments longer than a slot are split into
-// slot-sized chunks written / read at their file offsets.
+// slot-sized chunks written / read at their file offsets; a multi-chunk
+// fragment is written to <i>.frag.tmp and renamed into place once every chunk
+// succeeded, so a concurrent reader never sees it half written.
+//
+// Locking: host-buffer calls touch no ctx state and take no lock (ctx may be
+// NULL).  Device calls hold only the staging ring's own mutex, never the ctx
+// mutex, so a long store does not block uploads / downloads on the same ctx.
+// The file I/O runs on one process-wide pool of I/O threads.
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -75,7 +82,8 @@ size_t env_size(const char* name, size_t def, size_t lo, size_t hi) {
     return static_cast<size_t>(x);
 }
 
-// Fixed pool of I/O threads for one call.
+// Process-wide pool of I/O threads (shared by every call; a call waits on
+// its own latches, tasks never wait on each other).
 class Pool {
    public:
     explicit Pool(unsigned n) {
@@ -146,6 +154,11 @@ unsigned pool_threads() {
     return static_cast<unsigned>(env_size("DFS_STORE_THREADS", std::min(16u, hw), 1, 64));
 }
 
+Pool& io_pool() {
+    static Pool* p = new Pool(pool_threads());  // lives until exit (threads are detached at exit by the OS)
+    return *p;
+}
+
 std::string hex32(const uint8_t* d) {
     static const char* k = "0123456789abcdef";
     std::string s(64, '0');
@@ -214,6 +227,7 @@ struct Call {
         for (auto& s : st) s.store(DFS_OK, std::memory_order_relaxed);
     }
     std::string path(uint32_t i) const { return dir[i] + "/" + std::to_string(refs[i].index) + ".frag"; }
+    std::string tmp(uint32_t i) const { return path(i) + ".tmp"; }
     void fail(uint32_t i, int32_t code) {
         int32_t ok = DFS_OK;
         st[i].compare_exchange_strong(ok, code);
@@ -289,12 +303,12 @@ int finish(Call& c, int32_t* status, int rc) {
     return rc != DFS_OK ? rc : first;
 }
 
-int check_args(dfs_ctx* ctx, const char* root, const uint8_t* dig, const void* data, const dfs_frag_ref* refs,
-               uint32_t n, uint32_t flags) {
+int check_args(dfs_ctx* ctx, const char* root, const uint8_t* dig, uint32_t nfiles, const void* data,
+               const dfs_frag_ref* refs, uint32_t n, uint32_t flags) {
     if (!root || !*root || (n && (!dig || !refs))) return DFS_E_ARG;
     if ((flags & DFS_DEVICE_PTRS) && !ctx) return DFS_E_ARG;
     for (uint32_t i = 0; i < n; ++i)
-        if (refs[i].len && !data) return DFS_E_ARG;
+        if ((refs[i].len && !data) || refs[i].file >= nfiles) return DFS_E_ARG;
     return DFS_OK;
 }
 
@@ -302,12 +316,13 @@ int check_args(dfs_ctx* ctx, const char* root, const uint8_t* dig, const void* d
 
 extern "C" {
 
-int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, const uint8_t* data,
-                              const dfs_frag_ref* refs, uint32_t n, int32_t* status, uint32_t flags) {
-    if (int rc = check_args(ctx, node_root, file_digest, data, refs, n, flags)) return rc;
+int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, uint32_t nfiles,
+                              const uint8_t* data, const dfs_frag_ref* refs, uint32_t n, int32_t* status,
+                              uint32_t flags) {
+    if (int rc = check_args(ctx, node_root, file_digest, nfiles, data, refs, n, flags)) return rc;
     const bool dev = flags & DFS_DEVICE_PTRS;
     std::unique_lock<std::mutex> lk;
-    if (ctx) lk = std::unique_lock<std::mutex>(dfs::ctx_mutex(ctx));
+    if (dev) lk = std::unique_lock<std::mutex>(dfs::ctx_store_mutex(ctx));
     StoreStaging* stg = nullptr;
     if (dev) {
         if (hipSetDevice(dfs::ctx_device(ctx)) != hipSuccess) return DFS_E_HIP;
@@ -323,9 +338,15 @@ int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t
     std::vector<uint64_t> len(n);
     for (uint32_t i = 0; i < n; ++i) len[i] = refs[i].len;
 
-    Pool pool(pool_threads());
+    Pool& pool = io_pool();
+    // Chunks still to write per multi-chunk fragment (its .tmp is renamed
+    // into place by the writer of the last one).
+    std::vector<std::atomic<uint32_t>> chunks_left(n);
+    for (uint32_t i = 0; i < n; ++i)
+        chunks_left[i].store(len[i] > slot ? static_cast<uint32_t>((len[i] + slot - 1) / slot) : 0u,
+                             std::memory_order_relaxed);
     // Phase 1: directories (Files.createDirectories, SN:149 / 275), empty
-    // fragments, and pre-truncation of fragments written in several chunks.
+    // fragments, and the .tmp of fragments written in several chunks.
     {
         std::unordered_map<std::string, std::vector<uint32_t>> by_dir;
         for (uint32_t i = 0; i < n; ++i) by_dir[c.dir[i]].push_back(i);
@@ -340,7 +361,8 @@ int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t
                         continue;
                     }
                     if (len[i] == 0 || len[i] > slot) {
-                        int fd = ::open(c.path(i).c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+                        const std::string p = len[i] ? c.tmp(i) : c.path(i);
+                        int fd = ::open(p.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
                         if (fd < 0) c.fail(i, DFS_E_IO);
                         else ::close(fd);
                     }
@@ -353,15 +375,23 @@ int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t
 
     std::vector<std::vector<Chunk>> batches;
     plan_batches(c, len, slot, batches);
-    auto write_chunk = [&c, &len, slot](const Chunk& k, const uint8_t* src) {
+    auto write_chunk = [&c, &len, &chunks_left, slot](const Chunk& k, const uint8_t* src) {
         const bool whole = len[k.ref] <= slot;
-        int fd = ::open(c.path(k.ref).c_str(), O_WRONLY | O_CREAT | O_CLOEXEC | (whole ? O_TRUNC : 0), 0644);
+        const std::string p = whole ? c.path(k.ref) : c.tmp(k.ref);
+        int fd = ::open(p.c_str(), O_WRONLY | O_CREAT | O_CLOEXEC | (whole ? O_TRUNC : 0), 0644);
         if (fd < 0) {
             c.fail(k.ref, DFS_E_IO);
-            return;
+        } else {
+            if (!pwrite_all(fd, src, k.len, static_cast<off_t>(k.at))) c.fail(k.ref, DFS_E_IO);
+            if (::close(fd) != 0) c.fail(k.ref, DFS_E_IO);
         }
-        if (!pwrite_all(fd, src, k.len, static_cast<off_t>(k.at))) c.fail(k.ref, DFS_E_IO);
-        if (::close(fd) != 0) c.fail(k.ref, DFS_E_IO);
+        if (!whole && chunks_left[k.ref].fetch_sub(1, std::memory_order_acq_rel) == 1) {
+            if (c.st[k.ref].load() == DFS_OK) {
+                if (::rename(p.c_str(), c.path(k.ref).c_str()) != 0) c.fail(k.ref, DFS_E_IO);
+            } else {
+                ::unlink(p.c_str());
+            }
+        }
     };
 
     int rc = DFS_OK;
@@ -418,12 +448,13 @@ int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t
     return finish(c, status, rc);
 }
 
-int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, uint8_t* data,
-                             const dfs_frag_ref* refs, uint32_t n, uint64_t* out_len, int32_t* status, uint32_t flags) {
-    if (int rc = check_args(ctx, node_root, file_digest, data, refs, n, flags)) return rc;
+int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, uint32_t nfiles,
+                             uint8_t* data, const dfs_frag_ref* refs, uint32_t n, uint64_t* out_len, int32_t* status,
+                             uint32_t flags) {
+    if (int rc = check_args(ctx, node_root, file_digest, nfiles, data, refs, n, flags)) return rc;
     const bool dev = flags & DFS_DEVICE_PTRS;
     std::unique_lock<std::mutex> lk;
-    if (ctx) lk = std::unique_lock<std::mutex>(dfs::ctx_mutex(ctx));
+    if (dev) lk = std::unique_lock<std::mutex>(dfs::ctx_store_mutex(ctx));
     StoreStaging* stg = nullptr;
     if (dev) {
         if (hipSetDevice(dfs::ctx_device(ctx)) != hipSuccess) return DFS_E_HIP;
@@ -438,7 +469,7 @@ int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t*
     plan_dirs(c);
     std::vector<uint64_t> len(n, 0);
 
-    Pool pool(pool_threads());
+    Pool& pool = io_pool();
     const unsigned nt = pool_threads();
     // Phase 1: sizes (Files.exists + readAllBytes length, SN:465-466).
     {

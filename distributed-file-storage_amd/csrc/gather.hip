@@ -1,4 +1,4 @@
-// gather.hip — reassembly gather, synthetic data and digest compare.
+// gather.hip — reassembly gather and synthetic data.
 //
 // gather_kernel replaces handleDownload's ordered reassembly
 // (ByteArrayOutputStream.write at StorageNode.java:448, toByteArray at :451):
@@ -10,7 +10,7 @@
 namespace dfs {
 namespace {
 
-// Tile = P x 256 16-byte output chunks: chunk c of a fragment
+// Tile = P x 256 16-byte output chunks (P = 4): chunk c of a fragment
 // covers dst bytes [h + 16c, h + 16c + 16), a 16-byte aligned span (h = bytes
 // up to the first 16-aligned address, copy_items in dfs_gpu.cpp).  Every lane
 // issues the loads of all its chunks (dwordx4 + one dword when the source is
@@ -20,7 +20,8 @@ namespace {
 // byte is touched once.
 typedef uint32_t g32x4 __attribute__((ext_vector_type(4)));
 
-template <int P>  // 16-byte chunks per thread per tile
+constexpr int P = kGatherPer;  // 16-byte chunks per thread per tile
+
 __global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* __restrict__ jobs, uint32_t njobs,
                                                               uint64_t ntiles, uint8_t* __restrict__ out) {
     uint64_t t0, t1;
@@ -108,27 +109,11 @@ __global__ __launch_bounds__(kStreamBlock) void synth_kernel(uint8_t* __restrict
     }
 }
 
-__global__ void digest_compare_kernel(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, uint32_t n,
-                                      int32_t code, int32_t* __restrict__ status, uint32_t status_div) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint4* x = reinterpret_cast<const uint4*>(a + 32ull * i);
-    const uint4* y = reinterpret_cast<const uint4*>(b + 32ull * i);
-    const uint4 x0 = x[0], x1 = x[1], y0 = y[0], y1 = y[1];
-    const uint32_t d = (x0.x ^ y0.x) | (x0.y ^ y0.y) | (x0.z ^ y0.z) | (x0.w ^ y0.w) | (x1.x ^ y1.x) |
-                       (x1.y ^ y1.y) | (x1.z ^ y1.z) | (x1.w ^ y1.w);
-    if (d) atomicOr(status + i / status_div, code);
-}
-
 }  // namespace
 
-hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s,
-                         int per) {
+hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
-    if (per == 8)
-        hipLaunchKernelGGL(gather_kernel<8>, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
-    else
-        hipLaunchKernelGGL(gather_kernel<4>, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
+    hipLaunchKernelGGL(gather_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
     return hipGetLastError();
 }
 
@@ -137,14 +122,6 @@ hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uin
     if (ntiles == 0) return hipSuccess;
     hipLaunchKernelGGL(synth_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, dst, jobs, njobs, ntiles,
                        seed, file_off);
-    return hipGetLastError();
-}
-
-hipError_t launch_digest_compare(const uint8_t* a, const uint8_t* b, uint32_t n, int32_t code, int32_t* status,
-                                 uint32_t status_div, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(digest_compare_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, b, n, code, status,
-                       status_div);
     return hipGetLastError();
 }
 

@@ -16,11 +16,10 @@
 //  * Arbitrary byte offsets (fragment starts are not aligned): each lane
 //    loads 16 aligned dwords + 1 look-ahead dword per block and one
 //    v_perm_b32 per word does the funnel shift and the big-endian swap.
-//  * The next block is prefetched into a second register set while the
-//    current one is compressed (two register buffers, loop unrolled x2).
+//  * Blocks are fetched in pairs (one 128-byte line for line-aligned
+//    messages) and the next pair is in flight while the current pair is
+//    compressed (four register buffers, loop unrolled x4).
 #include "dfs_internal.h"
-
-#include <cstdlib>
 
 namespace dfs {
 namespace {
@@ -366,12 +365,12 @@ __device__ __forceinline__ uint32_t simd_key() {
 // token counters; all zeroed by the launcher before each launch.
 // ENC = the fused-Base64 instantiation (launched when the caller passes a
 // Base64 output; lanes flagged kShaB64 also write their message's Base64).
-template <bool ENC, int LOOP>
+template <bool ENC>
 __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
                                             uint32_t n, uint32_t split, uint32_t n_long, uint32_t cap,
                                             uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
-                                            uint32_t* __restrict__ queue, uint32_t* __restrict__ census,
-                                            uint32_t* __restrict__ state, char* __restrict__ b64) {
+                                            uint32_t* __restrict__ queue, uint32_t* __restrict__ state,
+                                            char* __restrict__ b64) {
     const uint32_t nitems = (n + 63u) >> 6;
     const uint32_t n_short = nitems - n_long;
     const uint32_t lane = threadIdx.x & 63u;
@@ -406,11 +405,6 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
         if (item == 0xffffffffu) break;
         if (item < n_long) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(0);
-        uint64_t t_start = 0, c_start = 0;
-        if (census) {
-            t_start = __builtin_amdgcn_s_memrealtime();
-            c_start = __builtin_amdgcn_s_memtime();
-        }
         const uint32_t gid = item * 64u + lane;
         // ENC: uniform trip count (the wave's longest message, in an SGPR).
         // A divergent loop exit inside the three-phase body made hipcc copy
@@ -479,7 +473,7 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                     const uint64_t start = 64ull * m.nfull - m.nfull % 3u;
                     enc_tail(pair, base + descs[gid].off, start, m.len, b64 + descs[gid].b64);
                 }
-            } else if (m.nfull && LOOP == 1) {
+            } else if (m.nfull) {
                 // Blocks are fetched in pairs (2j, 2j+1) requested back to
                 // back — one 128-byte line for line-aligned messages, so L2
                 // never has to keep a half-read line across a compression —
@@ -510,35 +504,6 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                     compress(st, D);
                     if (++k >= m.nfull) break;
                 }
-            } else if (m.nfull && LOOP == 0) {
-                uint32_t A[16], B[16], xa, xb;
-                load_block(m.p, m.sh, A, xa);
-                uint32_t k = 0;
-                for (;;) {
-                    // A holds block k; prefetch block k+1 (clamped) into B.
-                    load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, B, xb);
-                    to_be(A, xa, m.sel);
-                    compress(st, A);
-                    if (++k >= m.nfull) break;
-                    load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, A, xa);
-                    to_be(B, xb, m.sel);
-                    compress(st, B);
-                    if (++k >= m.nfull) break;
-                }
-            } else if (m.nfull) {
-                // One compression per iteration (half the code of LOOP 0):
-                // C = N is a register copy.
-                uint32_t C[16], N[16], xc, xn;
-                load_block(m.p, m.sh, C, xc);
-                for (uint32_t k = 0;;) {
-                    load_block(m.p + 16u * min(k + 1u, m.nfull - 1u), m.sh, N, xn);
-                    to_be(C, xc, m.sel);
-                    compress(st, C);
-                    if (++k >= m.nfull) break;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) C[i] = N[i];
-                    xc = xn;
-                }
             }
             if (m.flags & kShaPartial) {  // message continues in a later launch
                 uint4* s4 = reinterpret_cast<uint4*>(state + 8ull * m.out);
@@ -553,35 +518,22 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                 store_digest(st, m.out, split, out0, out1);
             }
         }
-        if (census && lane == 0u) {
-            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-            const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;  // shader clocks of this item
-            uint32_t* c = census + 4ull * item;
-            c[0] = hw_id();
-            c[1] = (xcc_id() << 28) | static_cast<uint32_t>(cyc > 0x0fffffffu ? 0x0fffffffu : cyc);
-            c[2] = static_cast<uint32_t>(t_start);
-            c[3] = static_cast<uint32_t>(t_end);
-        }
     }
 }
 
 #define DFS_SHA_ARGS                                                                                     \
     const uint8_t *__restrict__ base, const ShaDesc *__restrict__ descs, uint32_t n, uint32_t split,       \
         uint32_t n_long, uint32_t cap, uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,             \
-        uint32_t *__restrict__ queue, uint32_t *__restrict__ census, uint32_t *__restrict__ state,         \
-        char *__restrict__ b64
-// Plain (hash only).  LOOP = block-loop shape: 1 (default) pair-fetch with
-// four buffers, 0 two register buffers (unrolled x2), 2 one compression per
-// iteration (DFS_SHA_LOOP selects; experiment hook).  Measured, config 2
-// alone: 76.6 / 78.8 / 79.4 ms; beside Base64 (3 / 4 / 4 waves): 91.3 /
-// 93.1 / 93.9 ms.
-template <int LOOP>
+        uint32_t *__restrict__ queue, uint32_t *__restrict__ state, char *__restrict__ b64
+// Plain (hash only).  The pair-fetch block loop measured 76.6 ms alone on
+// config 2 (78.8 ms with two register buffers, 79.4 ms with one compression
+// per iteration); beside Base64 91.3 / 93.1 / 93.9 ms.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes(DFS_SHA_ARGS) {
-    sha256_body<false, LOOP>(base, descs, n, split, n_long, cap, out0, out1, queue, census, state, b64);
+    sha256_body<false>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64);
 }
 // Fused: fragment lanes flagged kShaB64 also write their Base64.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
-    sha256_body<true, 0>(base, descs, n, split, n_long, cap, out0, out1, queue, census, state, b64);
+    sha256_body<true>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64);
 }
 #undef DFS_SHA_ARGS
 
@@ -589,7 +541,7 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
-                         uint32_t* census, hipStream_t s, uint32_t* state, char* b64) {
+                         hipStream_t s, uint32_t* state, char* b64) {
     if (n == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
     if (e != hipSuccess) return e;
@@ -601,15 +553,10 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     if (b64) {
         hipLaunchKernelGGL(sha256_lanes_b64, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
-                           out0, out1, queue, census, state, b64);
+                           out0, out1, queue, state, b64);
     } else {
-        static const int loop = [] {
-            const char* v = std::getenv("DFS_SHA_LOOP");
-            return v ? std::atoi(v) : 1;
-        }();
-        auto k = loop == 1 ? sha256_lanes<1> : loop == 2 ? sha256_lanes<2> : sha256_lanes<0>;
-        hipLaunchKernelGGL(k, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long,
-                           cap, out0, out1, queue, census, state, nullptr);
+        hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
+                           out1, queue, state, nullptr);
     }
     return hipGetLastError();
 }

@@ -87,8 +87,8 @@ SIGNATURES = {
     "dfs_store_body_len": (_u64, [_u64, _u32, _u32, _u32]),
     "dfs_store_bodies_build": (_int, [_vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _u32]),
     "dfs_store_bodies_receive": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
-    "dfs_store_write_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _vp, _vp, _u32, _vp, _u32]),
-    "dfs_store_read_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _vp, _vp, _u32, _vp, _vp, _u32]),
+    "dfs_store_write_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _u32, _vp, _vp, _u32, _vp, _u32]),
+    "dfs_store_read_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _u32]),
 }
 
 _LIB = None

@@ -25,6 +25,16 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
+def _order_after_torch(engine) -> None:
+    """Device-mode store calls copy on the engine's ctx stream, which nothing
+    orders after torch's current stream: finish the producer (or consumer
+    fill) queued on torch's stream first.  A caller that set the
+    ctx stream to torch's own stream (engine.set_stream) is ordered already."""
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.current_stream(engine.device).synchronize()
+
+
 def make_refs(off: Sequence[int], length: Sequence[int], file: Sequence[int], index: Sequence[int]) -> np.ndarray:
     """dfs_frag_ref array: fragment `index[i]` of file `file[i]` at data + off[i]."""
     refs = np.zeros(len(off), dtype=FRAG_REF_DTYPE)
@@ -60,7 +70,10 @@ class FragmentStore:
         n = len(refs)
         status = np.zeros(max(n, 1), dtype=np.int32)
         dptr = ctypes.c_void_p(int(data)) if device else (ctypes.c_void_p(_ptr(data)) if data is not None else None)
-        rc = lib().dfs_store_write_fragments(self._ctx(device), self.root.encode(), _ptr(dig), dptr, _ptr(refs), n,
+        if device:
+            _order_after_torch(self.engine)
+        rc = lib().dfs_store_write_fragments(self._ctx(device), self.root.encode(), _ptr(dig), len(dig), dptr,
+                                             _ptr(refs), n,
                                              _ptr(status), L.DFS_DEVICE_PTRS if device else 0)
         if rc not in (L.DFS_OK, L.DFS_E_IO):
             check(rc, "dfs_store_write_fragments")
@@ -76,7 +89,10 @@ class FragmentStore:
         status = np.zeros(max(n, 1), dtype=np.int32)
         out_len = np.zeros(max(n, 1), dtype=np.uint64)
         dptr = ctypes.c_void_p(int(data)) if device else (ctypes.c_void_p(_ptr(data)) if data is not None else None)
-        rc = lib().dfs_store_read_fragments(self._ctx(device), self.root.encode(), _ptr(dig), dptr, _ptr(refs), n,
+        if device:
+            _order_after_torch(self.engine)
+        rc = lib().dfs_store_read_fragments(self._ctx(device), self.root.encode(), _ptr(dig), len(dig), dptr,
+                                            _ptr(refs), n,
                                             _ptr(out_len), _ptr(status), L.DFS_DEVICE_PTRS if device else 0)
         if rc not in (L.DFS_OK, L.DFS_E_IO, L.DFS_E_MISSING, L.DFS_E_ARG):
             check(rc, "dfs_store_read_fragments")

@@ -96,7 +96,7 @@ struct Node {
         const auto d = raw_id(fileId);
         dfs_frag_ref ref{0, b.size(), 0, static_cast<uint32_t>(index)};
         int32_t st = 0;
-        const int rc = dfs_store_write_fragments(nullptr, root.c_str(), d.data(), b.data(), &ref, 1, &st, 0);
+        const int rc = dfs_store_write_fragments(nullptr, root.c_str(), d.data(), 1, b.data(), &ref, 1, &st, 0);
         if (rc != DFS_OK) throw std::runtime_error(std::string("Files.write: ") + dfs_strerror(rc));
     }
     // tryLoadFragmentLocal (SN:463-469): the bytes, or nullopt if absent
@@ -111,7 +111,7 @@ struct Node {
         dfs_frag_ref ref{0, sz, 0, static_cast<uint32_t>(index)};
         uint64_t len = 0;
         int32_t st = 0;
-        const int rc = dfs_store_read_fragments(nullptr, root.c_str(), d.data(), b.data(), &ref, 1, &len, &st, 0);
+        const int rc = dfs_store_read_fragments(nullptr, root.c_str(), d.data(), 1, b.data(), &ref, 1, &len, &st, 0);
         if (st == DFS_E_MISSING) return std::nullopt;
         if (rc != DFS_OK) throw std::runtime_error(std::string("readAllBytes: ") + dfs_strerror(rc));
         b.resize(len);

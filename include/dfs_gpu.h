@@ -20,7 +20,15 @@
  *  - Digests are the raw 32-byte SHA-256; the Java side formats lowercase hex
  *    exactly as sha256Hex does (SN:607-609).
  *  - A ctx serialises its own calls (one mutex), so StorageNode's
- *    thread-per-connection handlers (SN:30) may share one ctx.
+ *    thread-per-connection handlers (SN:30) may share one ctx.  The stream
+ *    set by dfs_set_stream is ctx state (not per thread).  Asynchronous
+ *    (DFS_DEVICE_PTRS) calls reuse the ctx's device scratch: a call issued on
+ *    another stream than the previous one first waits (on the device) for
+ *    the previous call's scratch use, so switching streams is always safe.
+ *    An upload plan runs one launch at a time: two concurrent runs of the
+ *    same plan must be on the same stream.
+ *  - For many small concurrent requests use the batcher (dfs_batcher_*),
+ *    which coalesces them into one launch.
  *  - No CPU fallback: without a usable gfx950 device dfs_open fails with
  *    DFS_E_NODEV and nothing else runs.
  */
@@ -32,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DFS_ABI_VERSION 1
+#define DFS_ABI_VERSION 2
 
 /* Return codes. */
 #define DFS_OK 0
@@ -271,32 +279,39 @@ int dfs_store_bodies_receive(dfs_ctx* ctx, const char* bodies, const dfs_span* b
  * tryLoadFragmentLocal, SN:463-469).  node_root is the reference's dataRoot,
  * data/node-<id> (SN:20).  The manifest.json beside them is not written here.
  *   file_digest  host memory, 32 raw bytes per file; the directory name is
- *                its lowercase hex (sha256Hex, SN:607-609)
+ *                its lowercase hex (sha256Hex, SN:607-609); nfiles entries
  *   refs[i]      fragment i: bytes data + off, len of them (read: capacity),
- *                of file refs[i].file, fragment number refs[i].index
+ *                of file refs[i].file (< nfiles, else DFS_E_ARG before any
+ *                I/O), fragment number refs[i].index
  *   status[i]    0, DFS_E_IO (write / read failed), DFS_E_MISSING (read:
  *                no such file, tryLoadFragmentLocal returns null) or
  *                DFS_E_ARG (read: the file is longer than len)
  * Directories are created as Files.createDirectories does (SN:149, 275);
- * files are created or truncated (Files.write's default options).  With
+ * files are created or truncated (Files.write's default options); a
+ * fragment larger than one staging slot (DFS_STORE_SLOT_MB, 64 MiB) is
+ * written to <index>.frag.tmp and renamed into place when complete.  With
  * DFS_DEVICE_PTRS `data` is device memory: the bytes move through the ctx's
  * pinned staging ring (HBM <-> host on the ctx stream, overlapped with the
- * file I/O of a host thread pool).  Without it `data` is host memory and
- * ctx may be NULL (pure file I/O).  Returns DFS_OK or the first failing
- * status; every ref is attempted.  Synchronous. */
+ * file I/O of a process-wide thread pool).  Ordering: the copies run on the
+ * ctx stream only, so work that produces `data` (write) or reads it back
+ * (read) on another stream must be ordered by the caller (dfs_set_stream to
+ * that stream, or synchronise it first).  Device calls hold the staging
+ * ring's own lock, not the ctx lock.  Without DFS_DEVICE_PTRS `data` is host
+ * memory, no lock is taken and ctx may be NULL (pure file I/O).  Returns
+ * DFS_OK or the first failing status; every ref is attempted.  Synchronous. */
 typedef struct dfs_frag_ref {
     uint64_t off;
     uint64_t len;
     uint32_t file;
     uint32_t index;
 } dfs_frag_ref;
-int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest,
+int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, uint32_t nfiles,
                               const uint8_t* data, const dfs_frag_ref* refs, uint32_t n, int32_t* status,
                               uint32_t flags);
 /* out_len[i] = bytes of fragment i (the file's size) when status[i] is 0. */
-int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, uint8_t* data,
-                             const dfs_frag_ref* refs, uint32_t n, uint64_t* out_len, int32_t* status,
-                             uint32_t flags);
+int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t* file_digest, uint32_t nfiles,
+                             uint8_t* data, const dfs_frag_ref* refs, uint32_t n, uint64_t* out_len,
+                             int32_t* status, uint32_t flags);
 
 /* ---- prepared upload (descriptor build once, run many; device pointers) --- */
 /* flags: DFS_LAYOUT_FRAG_MAJOR stores the Base64 of fragment i of every file

@@ -122,17 +122,25 @@ def test_bad_arguments(tmp_path):
     refs = make_refs([0], [4], [0], [0])
     st = np.zeros(1, dtype=np.int32)
     # device pointers without a ctx, NULL root, NULL data with a non-empty ref
-    assert lib.dfs_store_write_fragments(None, str(tmp_path).encode(), dig.ctypes.data, None, refs.ctypes.data, 1,
+    assert lib.dfs_store_write_fragments(None, str(tmp_path).encode(), dig.ctypes.data, 1, None, refs.ctypes.data, 1,
                                          st.ctypes.data, L.DFS_DEVICE_PTRS) == L.DFS_E_ARG
-    assert lib.dfs_store_write_fragments(None, None, dig.ctypes.data, None, refs.ctypes.data, 1, st.ctypes.data,
+    assert lib.dfs_store_write_fragments(None, None, dig.ctypes.data, 1, None, refs.ctypes.data, 1, st.ctypes.data,
                                          0) == L.DFS_E_ARG
-    assert lib.dfs_store_read_fragments(None, str(tmp_path).encode(), dig.ctypes.data, None, refs.ctypes.data, 1,
+    assert lib.dfs_store_read_fragments(None, str(tmp_path).encode(), dig.ctypes.data, 1, None, refs.ctypes.data, 1,
                                         None, st.ctypes.data, 0) == L.DFS_E_ARG
+    # a ref naming a file past the digest table: rejected before any I/O
+    data4 = np.zeros(4, dtype=np.uint8)
+    bad = make_refs([0], [4], [1], [0])
+    assert lib.dfs_store_write_fragments(None, str(tmp_path).encode(), dig.ctypes.data, 1, data4.ctypes.data,
+                                         bad.ctypes.data, 1, st.ctypes.data, 0) == L.DFS_E_ARG
+    assert lib.dfs_store_read_fragments(None, str(tmp_path).encode(), dig.ctypes.data, 1, data4.ctypes.data,
+                                        bad.ctypes.data, 1, None, st.ctypes.data, 0) == L.DFS_E_ARG
+    assert not any(tmp_path.iterdir())
     # a path component that is a file -> DFS_E_IO (createDirectories throws)
     blocker = tmp_path / "blk"
     blocker.write_bytes(b"")
     data = np.zeros(4, dtype=np.uint8)
-    assert lib.dfs_store_write_fragments(None, str(blocker).encode(), dig.ctypes.data, data.ctypes.data,
+    assert lib.dfs_store_write_fragments(None, str(blocker).encode(), dig.ctypes.data, 1, data.ctypes.data,
                                          refs.ctypes.data, 1, st.ctypes.data, 0) == L.DFS_E_IO
     assert st[0] == L.DFS_E_IO
 

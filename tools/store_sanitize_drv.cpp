@@ -32,8 +32,8 @@ int main() {
     std::vector<int32_t> st(refs.size());
     std::vector<uint64_t> len(refs.size());
     for (int it = 0; it < 3; ++it) {
-        int rc = dfs_store_write_fragments(nullptr, dir.c_str(), dig.data(), data.data(), refs.data(), refs.size(), st.data(), 0);
-        int rc2 = dfs_store_read_fragments(nullptr, dir.c_str(), dig.data(), back.data(), refs.data(), refs.size(), len.data(), st.data(), 0);
+        int rc = dfs_store_write_fragments(nullptr, dir.c_str(), dig.data(), uint32_t(nf), data.data(), refs.data(), refs.size(), st.data(), 0);
+        int rc2 = dfs_store_read_fragments(nullptr, dir.c_str(), dig.data(), uint32_t(nf), back.data(), refs.data(), refs.size(), len.data(), st.data(), 0);
         if (rc || rc2 || back != data) { std::printf("FAIL %d %d\n", rc, rc2); return 1; }
     }
     std::printf("store sanitize driver OK (%zu refs, %llu bytes)\n", refs.size(), (unsigned long long)pos);
