@@ -4,32 +4,45 @@
 One step = one pass of handleUpload's fragment pipeline (StorageNode.java
 :118-189) over one batch of synthetic files resident in HBM: fileId SHA-256
 (:127), N-way split (:138-157), per-fragment SHA-256 (:159) and the Base64 of
-every fragment (:636) — all in the gfx950 kernels of libdfsgpu.so.
+every fragment (:636) — all in the gfx950 kernels of libdfsgpu.so — and, on
+N > 1 GPUs, the replica placement of that Base64 (sendFragmentsToPeers,
+:195-224) over RCCL / xGMI.
 
-Default workload = BASELINE.json configs[1]: 65,536 files x 1 MiB per GPU,
-N = 5 fragments.  With --gpus N (launched one rank per GPU by
-torch.distributed.run) every rank processes its own shard of files (weak
-scaling, no data-path collective); `value` = file bytes of all ranks / the
-slowest rank's time.  Rank 0 prints ONE JSON line.
+Workloads (BASELINE.json configs):
+  N = 1  configs[1]: 65,536 files x 1 MiB, N = 5 fragments (default).
+  N > 1  configs[2]: its per-GPU shard, 131,072 files x 256 KiB, N = 8
+         fragments per GPU (1M files on 8 GPUs), node k hosted by GPU k mod W.
+         The step is upload + placement: the files are processed in chunks
+         and chunk c's placement runs on a comm stream beside chunk c+1's
+         hashing (--placement star: the reference's own fan-out as one
+         all-to-all; ring: primary scatter + replica step g -> g-1).
+`python bench.py --gpus N` launches its own N ranks (torch.distributed.run)
+when WORLD_SIZE is not set; rank 0 prints ONE JSON line and the exit code is
+non-zero if any leg failed or mismatched.
 
 Extra objects on the line:
   roofline      dominant kernel (multi-message SHA-256) vs the int32-VALU peak,
                 timed with HIP events on its own stream inside the timed loop
   roofline_b64  the Base64 encode kernel vs the HBM peak
   cpu_baseline  CPU restatement (OpenSSL SHA-NI SHA-256 + scalar Base64, one
-                file per thread) on a bounded sample, rank 0, N = 1 only
+                file per thread) on a bounded sample, rank 0, N = 1 only;
+                `download` inside it: the download path on the CPU
   download      handleDownload over the same files: Base64 decode into place +
                 fragment / fileId SHA-256 verify, and the raw-fragment gather
   wire          storeFragments request bodies built on the device, then
                 received (parse + decode + SHA-256) on the device
   store         on-disk fragment store: node 1's fragments HBM -> disk -> HBM
-  replication   N > 1: ring and all-to-all placement over RCCL, degraded read
+  placement     N > 1: ring and star xGMI rates, compute-only rate, the
+                degraded read (config 5: last GPU offline, fetch + decode +
+                verify + reassembly)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,6 +63,10 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 
 
+class LegError(RuntimeError):
+    pass
+
+
 def sha_blocks(n: int) -> int:
     return n // 64 + (1 if n % 64 < 56 else 2)
 
@@ -59,14 +76,18 @@ def split(S: int, N: int):
     return [base + (1 if i < rem else 0) for i in range(N)]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--files", type=int, default=65536, help="files per GPU")
-    ap.add_argument("--file-size", type=int, default=1 << 20)
-    ap.add_argument("--nfrag", type=int, default=5)
+    ap.add_argument("--config", type=int, default=0, choices=(0, 2, 3, 4),
+                    help="0 (default): configs[1] at N=1, configs[2]'s per-GPU shard at N>1; 2: BASELINE "
+                         "configs[1]; 3: configs[2]'s per-GPU shard (131,072 x 256 KiB, N=8); 4: configs[3], the "
+                         "long-fragment skew (1,024 x 256 MiB, N=5) streamed through HBM, its own JSON line")
+    ap.add_argument("--files", type=int, default=0, help="files per GPU (0 = the config's)")
+    ap.add_argument("--file-size", type=int, default=0)
+    ap.add_argument("--nfrag", type=int, default=0)
     ap.add_argument("--mode", choices=("fused", "kernels", "serial"), default="kernels",
                     help="kernels: SHA and Base64 kernels on two streams (default); fused: Base64 "
                          "written by the SHA fragment lanes; serial: the two kernels on one stream")
@@ -76,166 +97,158 @@ def parse():
     ap.add_argument("--b64-steps", type=int, default=3, help="steps of the standalone Base64 leg")
     ap.add_argument("--frag-only-steps", type=int, default=3, help="steps of the fragment-only (no fileId) leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work (upload leg)")
     ap.add_argument("--verify", type=int, default=8, help="files spot-checked against the oracle (rank 0)")
-    ap.add_argument("--no-replicate", action="store_true", help="N>1: skip the placement / degraded-read leg")
-    ap.add_argument("--rep-files", type=int, default=8192, help="files per GPU in the placement leg")
-    ap.add_argument("--rep-steps", type=int, default=3)
+    ap.add_argument("--placement", choices=("star", "ring"), default="star",
+                    help="N>1: placement inside the timed step (the other one is timed beside it)")
+    ap.add_argument("--chunks", type=int, default=4, help="N>1: file chunks pipelined through compute + placement")
     ap.add_argument("--no-download", action="store_true", help="skip the download/verify leg")
     ap.add_argument("--dl-steps", type=int, default=2)
-    ap.add_argument("--dl-chunks", type=int, default=0,
-                    help="> 0: also time the chunked 2-context download (slower: see DESIGN §9)")
     ap.add_argument("--wire-files", type=int, default=16384, help="files in the storeFragments body leg")
     ap.add_argument("--no-wire", action="store_true", help="skip the storeFragments body leg")
     ap.add_argument("--store-files", type=int, default=2048, help="files in the on-disk fragment store leg")
     ap.add_argument("--no-store", action="store_true", help="skip the on-disk fragment store leg")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4),
-                    help="2: BASELINE configs[1] (default bench line); 3: configs[2]'s per-GPU shard "
-                         "(131,072 x 256 KiB, N=8 per GPU; 1M files on 8 GPUs); 4: configs[3], the long-fragment "
-                         "skew (1,024 x 256 MiB, N=5) streamed through HBM in chunks, its own JSON line")
     ap.add_argument("--long-files", type=int, default=1024)
     ap.add_argument("--long-size", type=int, default=256 << 20)
     ap.add_argument("--long-chunk", type=int, default=192 * 87381, help="bytes per file per chunk (x192)")
-    args = ap.parse_args()
-    if args.config == 3:  # BASELINE configs[2]: 1M files x 256 KiB sharded by file over 8 GPUs, N = 8
-        args.files, args.file_size, args.nfrag = 131072, 256 << 10, 8
+    ap.add_argument("--dry-run", action="store_true",
+                    help="harness check without a GPU (gloo, CPU tensors): launcher, rendezvous, timing and the "
+                         "placement schedules; prints a line marked dry_run, never a measurement")
+    return ap.parse_args(argv)
+
+
+def resolve_config(args, world: int) -> None:
+    cfg = args.config or (2 if world == 1 else 3)
+    args.config = cfg
+    if cfg == 3:  # BASELINE configs[2]: 1M files x 256 KiB sharded by file over 8 GPUs, N = 8
+        F, S, N = 131072, 256 << 10, 8
         args.wire_files = min(args.wire_files, 65536)
-    return args
+    else:
+        F, S, N = 65536, 1 << 20, 5
+    args.files = args.files or F
+    args.file_size = args.file_size or S
+    args.nfrag = args.nfrag or N
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks (one per GPU) with
+    torch.distributed.run as a child process.  Runs before this process
+    touches the GPU; returns the child's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the oracle's C restatement on the host cores
+# ---------------------------------------------------------------------------
+def host_cpu_info():
+    """Cores this process may use and what they are: nproc (the machine),
+    the affinity set, the cgroup CPU quota (a GPU box gives a process a
+    share of the machine), the lscpu model name."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    info["affinity"] = aff
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    info["cgroup_cpu_quota"] = quota
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    info["model"] = model
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return info, usable
 
 
 def cpu_baseline(args, log):
-    """Oracle leg: C restatement on the host cores, bounded sample."""
+    """Oracle leg: C restatement on the host cores, bounded sample, on every
+    core this process may use (one file per thread, thread-per-connection
+    SN:30), plus one connection handler alone and the download path."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # noqa: E402  (test infrastructure, checker/baseline only)
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+    info, threads = host_cpu_info()
     S, N = args.file_size, args.nfrag
-    # calibrate: 2 files per thread
     secs, _, _ = O.cpu_upload_bench(2 * threads, S, N, threads, use_openssl=True)
     kind_sha = "openssl"
     if secs < 0:
         secs, _, _ = O.cpu_upload_bench(2 * threads, S, N, threads, use_openssl=False)
         kind_sha = "scalar"
+    ossl = kind_sha == "openssl"
     per_file = max(secs, 1e-6) / 2.0  # seconds per file per thread
-    nfiles = int(max(threads, min(200000, args.cpu_seconds / per_file * threads)))
-    secs, _, _ = O.cpu_upload_bench(nfiles, S, N, threads, use_openssl=(kind_sha == "openssl"))
+    nfiles = int(max(threads, min(400000, args.cpu_seconds / per_file * threads)))
+    secs, _, _ = O.cpu_upload_bench(nfiles, S, N, threads, use_openssl=ossl)
+    if secs <= 0:
+        raise LegError(f"cpu upload baseline failed ({secs})")
     gbs = nfiles * S / secs / 1e9
-    log(f"cpu baseline: {nfiles} files x {S} B on {threads} threads: {secs:.2f} s -> {gbs:.3f} GB/s")
-    # one connection-handler thread alone (SURVEY §8d: 1-thread and all-core)
+    log(f"cpu baseline: {nfiles} files x {S} B on {threads} threads ({info}): {secs:.2f} s -> {gbs:.3f} GB/s")
     n1 = int(max(1, min(20000, 3.0 / per_file)))
-    secs1, _, _ = O.cpu_upload_bench(n1, S, N, 1, use_openssl=(kind_sha == "openssl"))
+    secs1, _, _ = O.cpu_upload_bench(n1, S, N, 1, use_openssl=ossl)
     gbs1 = n1 * S / secs1 / 1e9
-    log(f"cpu baseline: {n1} files on 1 thread: {secs1:.2f} s -> {gbs1:.3f} GB/s")
+    # download path: decode + fragment verify + ordered append + fileId verify
+    d_cal = O.cpu_download_bench(threads, S, N, threads, ossl)
+    if d_cal <= 0:
+        raise LegError(f"cpu download baseline failed ({d_cal})")
+    nd = int(max(threads, min(400000, 0.5 * args.cpu_seconds / max(d_cal, 1e-6) * threads)))
+    d_secs = O.cpu_download_bench(nd, S, N, threads, ossl)
+    if d_secs <= 0:
+        raise LegError(f"cpu download baseline failed ({d_secs})")
+    d_gbs = nd * S / d_secs / 1e9
+    log(f"cpu baseline download: {nd} files on {threads} threads: {d_secs:.2f} s -> {d_gbs:.3f} GB/s")
+    sha_txt = "OpenSSL SHA256 (SHA-NI), approximating the HotSpot intrinsic" if ossl else "scalar C SHA-256"
     return {"value": round(gbs, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{nfiles} synthetic files x {S} B, N={N}: fileId + fragment SHA-256 "
-                      f"({'OpenSSL SHA256 (SHA-NI), approximating HotSpot intrinsic' if kind_sha == 'openssl' else 'scalar C'})"
-                      f" + scalar Base64, one file per thread (thread-per-connection, SN:30); "
-                      f"CPU proxy, not Java (no JDK on the box)",
-            "seconds": round(secs, 3), "single_thread_value": round(gbs1, 4), "single_thread_files": n1}
+            "sample": f"{nfiles} synthetic files x {S} B, N={N}: fileId + fragment SHA-256 ({sha_txt}) + scalar "
+                      f"Base64, one file per thread (thread-per-connection, SN:30), {threads} threads; CPU proxy, "
+                      f"not Java (no JDK on the box)",
+            "host": info, "seconds": round(secs, 3),
+            "single_thread_value": round(gbs1, 4), "single_thread_files": n1,
+            "download": {"value": round(d_gbs, 4), "unit": "GB/s", "cores": threads, "files": nd,
+                         "seconds": round(d_secs, 3),
+                         "sample": "per file: table-driven Base64 decode of each fragment (SN:281), SHA-256 vs the "
+                                   "upload digest (SN:282, 250-257), ordered append (SN:448), SHA-256 vs fileId "
+                                   "(SN:454); same files, one file per thread"}}
 
 
-def replication_leg(args, eng, files, S, N, dev, log):
-    """N>1 only: place a bounded sample of this rank's fragments on the GPUs
-    hosting their nodes (primary scatter + replica step over RCCL/xGMI,
-    dfs_amd.placement), then run config 5's degraded download with the last
-    rank offline: fetch from the surviving holders, Base64-decode into place,
-    per-fragment and fileId SHA-256 verify (dfs_download_batch).  Timed
-    separately from the compute steps; returns a dict for the JSON line."""
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-    import dfs_amd
-    from dfs_amd import placement as P
-    from dfs_amd.engine import download_device
-    world, me = dist.get_world_size(), dist.get_rank()
-    R = min(args.files, args.rep_files)
-    spans = np.stack([np.arange(R, dtype=np.uint64) * np.uint64(S), np.full(R, S, dtype=np.uint64)], axis=1)
-    plan = dfs_amd.UploadPlan(eng, spans, N, frag_major=True)
-    fd = torch.empty(R * 32, dtype=torch.uint8, device=dev)
-    frd = torch.empty(R * N * 32, dtype=torch.uint8, device=dev)
-    b64 = torch.empty(plan.b64_total, dtype=torch.uint8, device=dev)
-    plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), dfs_amd.DFS_SERIAL)
-    torch.cuda.synchronize(dev)
-    offs = plan.b64_offsets()
-    group_off = [int(offs[i]) for i in range(N)] + [int(offs[-1])]
-
-    def timed(fn, reps):
-        fn()  # warm-up
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            r = fn()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        return r, float(tt.item()) / reps
-
-    (held, table), t_up = timed(lambda: P.exchange_upload(b64, group_off, N), args.rep_steps)
-    sent = sum(table[me][f] for f in range(N) if P.node_gpu(f, world) != me)
-    sent += sum(sum(table[r][f] for r in range(world)) for f in range(N)
-                if P.node_gpu(f, world) == me and P.node_gpu(P.fragment_holders(f, N)[1], world) != me)
-    sent_t = torch.tensor([sent], dtype=torch.float64, device=dev)
-    dist.all_reduce(sent_t)
-    ok_ex = all(len(held[f][0]) == sum(table[r][f] for r in range(world)) for f in P.gpu_fragments(me, N, world))
-
-    # The reference's star fan-out (SN:195-205) as one all-to-all: every link busy at once.
-    (held_s, _t), t_star = timed(lambda: P.exchange_upload_star(b64, group_off, N), args.rep_steps)
-    ok_ex = ok_ex and all(torch.equal(held_s[f][0], held[f][0]) for f in P.gpu_fragments(me, N, world))
-    need = [P.gpu_fragments(g, N, world) for g in range(world)]
-    sent_s = sum(table[me][f] for g in range(world) if g != me for f in need[g])
-    sent_st = torch.tensor([sent_s], dtype=torch.float64, device=dev)
-    dist.all_reduce(sent_st)
-    del held_s
-
-    offline = {world - 1}
-    fetched, t_fetch = timed(lambda: P.exchange_download(held, table, N, offline=offline, device=dev), args.rep_steps)
-    result = {"files_per_gpu": R, "nodes": N, "node_to_gpu": "node k on GPU k mod W",
-              "upload_exchange_ms": round(t_up * 1e3, 3),
-              "upload_exchange_gbps_per_gpu": round(sent_t.item() / world / t_up / 1e9, 2),
-              "star_exchange_ms": round(t_star * 1e3, 3),
-              "star_exchange_gbps_per_gpu": round(sent_st.item() / world / t_star / 1e9, 2),
-              "exchange_sizes_ok": bool(ok_ex), "offline_gpu": world - 1,
-              "degraded_fetch_ms": round(t_fetch * 1e3, 3)}
-    status_ok = True
-    if me not in offline:
-        # one contiguous Base64 buffer, spans per (file, fragment)
-        groups = [fetched[f] for f in range(N)]
-        status_ok = all(g is not None for g in groups)
-        if status_ok:
-            blob = torch.cat(groups)
-            msp = P.frag_major_spans([S] * R, N)
-            out = torch.empty(R * S, dtype=torch.uint8, device=dev)
-            file_len = np.full(R, S, dtype=np.uint64)
-            file_off = np.arange(R, dtype=np.uint64) * np.uint64(S)
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            status = download_device(eng, blob.data_ptr(), msp, R, N, file_len, frd.data_ptr(), fd.data_ptr(),
-                                     out.data_ptr(), file_off)
-            t_dl = time.perf_counter() - t0
-            status_ok = bool((status == 0).all()) and bool(torch.equal(out, files[:R * S]))
-            result["degraded_download_ms"] = round(t_dl * 1e3, 3)
-            result["degraded_download_gbps"] = round(R * S / t_dl / 1e9, 2)
-    flag = torch.tensor([1 if status_ok else 0], dtype=torch.int32, device=dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-    result["degraded_download_ok"] = bool(flag.item())
-    plan.close()
-    return result
-
-
+# ---------------------------------------------------------------------------
+# Side legs (N = 1)
+# ---------------------------------------------------------------------------
 def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
     """handleDownload's verify path (SN:399-461) plus north_star's per-fragment
     check, over this GPU's whole upload: Base64-decode every fragment straight
     into its file offset (fused gather, SN:448-451), per-fragment SHA-256 vs the
     upload-time digests, fileId SHA-256 re-verify (SN:454-458) — one
-    dfs_download_batch on device buffers.  Returns a dict for the JSON line."""
+    dfs_download_batch on device buffers."""
     import numpy as np
     import torch
-    from dfs_amd.engine import download_device
+    from dfs_amd.engine import download_device, reassemble_device
     msp = plan.b64_spans([S] * F)
     file_len = np.full(F, S, dtype=np.uint64)
     file_off = np.arange(F, dtype=np.uint64) * np.uint64(S)
@@ -260,14 +273,9 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
         ok = ok and bool((st == 0).all())
     eng.set_profiling(False)
     ok = ok and bool(torch.equal(out, files[:F * S]))
-    pipe = None
-    if args.dl_chunks > 0:
-        pipe = pipelined_download(args, eng, files, fd, frd, b64, msp, out, S, N, F, dev)
-        ok = ok and pipe.get("ok", False)
     # Raw-fragment reassembly (SN:419-451, fragments fetched as raw bytes,
-    # :513-514): gather the fragments of every file (spans of the upload
-    # buffer) into `out`, then the fileId re-verify (:454-458).
-    from dfs_amd.engine import reassemble_device
+    # :513-514): gather the fragments of every file into `out`, then the
+    # fileId re-verify (:454-458).
     out.zero_()
     lens = np.array(split(S, N), dtype=np.uint64)
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
@@ -292,79 +300,27 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
     dec_bytes = int(msp[:, 1].sum()) + F * S  # Base64 read + bytes written
     log(f"download: {F} files, device {dev_ms:.1f} ms (decode {dec_ms:.1f}, sha {np.mean(sha):.1f}), "
         f"raw gather {gat_ms:.1f} ms, ok={ok}")
+    if not ok:
+        raise LegError("download leg: status or bytes differ")
     return {"files_per_gpu": F, "device_ms": round(dev_ms, 3), "wall_ms": round(float(np.mean(wall)) * 1e3, 3),
             "gbps": round(F * S / (dev_ms / 1e3) / 1e9, 2),
             "decode_ms": round(dec_ms, 3), "decode_gbs": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
             "decode_frac_hbm": round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "sha_ms": round(float(np.mean(sha)), 3),
             "gather_ms": round(gat_ms, 3), "gather_gbs": round(gat_gbs, 1),
-            "gather_frac_hbm": round(gat_gbs / HBM_PEAK_GBS, 4), "ok": ok, **({"pipelined": pipe} if pipe else {}),
+            "gather_frac_hbm": round(gat_gbs / HBM_PEAK_GBS, 4), "ok": ok,
             "note": "wall_ms includes host-side job planning per call; gbps = file bytes / device time"}
-
-
-def pipelined_download(args, eng, files, fd, frd, b64, msp, out, S, N, F, dev):
-    """Server-style download: the same F files as chunks over two contexts on
-    two host threads (two connection handlers, SN:30, sharing a GPU), so one
-    chunk's verify SHA-256 runs beside the next chunk's Base64 decode.  The
-    second thread starts with a half chunk so the two do not run in lockstep.
-    Wall clock over the whole set, host planning included."""
-    import threading
-    import numpy as np
-    import torch
-    import dfs_amd
-    from dfs_amd.engine import download_device
-    K = max(2, args.dl_chunks)
-    step = F // K
-    bounds = [0, step // 2] + [step // 2 + step * i for i in range(1, K)] + [F]
-    bounds = sorted(set(b for b in bounds if 0 <= b <= F))
-    chunks = list(zip(bounds[:-1], bounds[1:]))
-    file_len = np.full(F, S, dtype=np.uint64)
-    file_off = np.arange(F, dtype=np.uint64) * np.uint64(S)
-    eng2 = dfs_amd.FragmentEngine(dev.index or 0)
-    engines = [eng, eng2]
-    ok = [True]
-
-    def run(t):
-        for c, (a, b) in enumerate(chunks):
-            if c % 2 != t:
-                continue
-            st = download_device(engines[t], b64.data_ptr(), msp[a * N:b * N], b - a, N, file_len[a:b],
-                                 frd.data_ptr() + a * N * 32, fd.data_ptr() + a * 32, out.data_ptr(), file_off[a:b])
-            ok[0] = ok[0] and bool((st == 0).all())
-
-    def once():
-        ths = [threading.Thread(target=run, args=(t,)) for t in (0, 1)]
-        t0 = time.perf_counter()
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        return time.perf_counter() - t0
-
-    try:
-        once()
-        out.zero_()
-        torch.cuda.synchronize(dev)
-        walls = [once() for _ in range(max(1, args.dl_steps))]
-        torch.cuda.synchronize(dev)
-        good = ok[0] and bool(torch.equal(out, files[:F * S]))
-    finally:
-        eng2.close()
-    ms = float(np.mean(walls)) * 1e3
-    return {"chunks": len(chunks), "contexts": 2, "wall_ms": round(ms, 3),
-            "gbps": round(F * S / (ms / 1e3) / 1e9, 2), "ok": good}
 
 
 def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
     """storeFragments request bodies on the device (SN:195-205 + 629-642):
     node 1 (0-based 0) uploads; for each sampled file the N-1 peer bodies
     {"fileId":..,"fragments":[{k},{k+1}]} with the Base64 encoded straight
-    from the file bytes into the body.  Timed with HIP events; the first and
-    last files are checked byte-for-byte against the oracle's
-    buildFragmentsJson.  Returns a dict for the JSON line."""
+    from the file bytes into the body; then received on the device."""
     import numpy as np
     import torch
-    from dfs_amd.engine import store_bodies_layout, store_bodies_device
+    from dfs_amd.engine import (store_bodies_device, store_bodies_layout, store_receive_device,
+                                store_receive_out_bytes)
     R = min(F, args.wire_files)
     spans = np.stack([np.arange(R, dtype=np.uint64) * np.uint64(S), np.full(R, S, dtype=np.uint64)], axis=1)
     body_off = store_bodies_layout(eng, spans, N, 0)
@@ -388,7 +344,6 @@ def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import hashlib
         import oracle as O  # checker only
-        host = None
         for f in sorted({0, R - 1}):
             data = files[f * S:(f + 1) * S].cpu().numpy().tobytes()
             fid = hashlib.sha256(data).hexdigest()
@@ -398,10 +353,8 @@ def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
                 o = int(body_off[f * (N - 1) + j])
                 ok &= bodies[o:o + len(want)].cpu().numpy().tobytes() == want
     # Receiver side (handleInternalStoreFragments, SN:265-293) over the same
-    # bodies: device parse, decode of both entries, SHA-256 of each; the
-    # digests must equal the upload-time fragment digests (the sender's check,
-    # SN:248-257).  Synchronous call, wall-clock timed.
-    from dfs_amd.engine import store_receive_device, store_receive_out_bytes
+    # bodies; the digests must equal the upload-time fragment digests (the
+    # sender's check, SN:248-257).  Synchronous call, wall-clock timed.
     lens = split(S, N)
     blen = np.array([139 + 4 * ((lens[k] + 2) // 3) + 4 * ((lens[(k + 1) % N] + 2) // 3) for k in range(1, N)],
                     dtype=np.uint64)
@@ -428,14 +381,15 @@ def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
     raw_read = sum(lens[k] + lens[(k + 1) % N] for k in range(1, N))
     moved = R * (body_bytes + raw_read)
     ms = float(np.mean(tot))
-    log(f"wire: {R} files x {N - 1} storeFragments bodies, {ms:.1f} ms, ok={ok}")
+    log(f"wire: {R} files x {N - 1} storeFragments bodies, {ms:.1f} ms, ok={ok}, receive ok={rok}")
     del bodies
+    if not (ok and rok):
+        raise LegError(f"wire leg: bodies ok={ok} receive ok={rok}")
     return {"files": R, "bodies": R * (N - 1), "uploader_node": 1, "ms": round(ms, 3),
             "encode_ms": round(float(np.mean(enc)), 3), "body_gbs": round(R * body_bytes / (ms / 1e3) / 1e9, 1),
             "hbm_gbs": round(moved / (ms / 1e3) / 1e9, 1), "hbm_frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-            "ok": bool(ok),
-            "receive_wall_ms": round(recv_ms, 3), "receive_body_gbs": round(R * body_bytes / (recv_ms / 1e3) / 1e9, 1),
-            "receive_ok": rok,
+            "ok": bool(ok), "receive_wall_ms": round(recv_ms, 3),
+            "receive_body_gbs": round(R * body_bytes / (recv_ms / 1e3) / 1e9, 1), "receive_ok": rok,
             "note": "bodies byte-identical to buildFragmentsJson (SN:629-642); hbm_gbs = raw fragment bytes read "
                     "+ body bytes written per second; receive = device parse + decode + SHA-256 of every entry "
                     "(synchronous call, wall clock incl. host job planning), digests == upload-time fragment "
@@ -446,9 +400,7 @@ def store_leg(args, eng, files, fd, S, N, F, dev, log):
     """On-disk fragment store (SN:147-166 upload save, SN:463-469 local load):
     node 1 (0-based 0) keeps fragments {0, 1} of every sampled file; they go
     HBM -> pinned ring -> <tmp>/node-1/<fileId>/fragments/<i>.frag and back
-    into HBM (dfs_store_write_fragments / dfs_store_read_fragments).  The
-    read follows the write, so it is a page-cache rate (the box gives no way
-    to drop caches).  Checked: every byte read back equals the file bytes."""
+    into HBM.  The read follows the write, so it is a page-cache rate."""
     import shutil
     import tempfile
     import numpy as np
@@ -462,16 +414,12 @@ def store_leg(args, eng, files, fd, S, N, F, dev, log):
     ln = [lens[i] for _ in range(R) for i in keep]
     fi = [f for f in range(R) for _ in keep]
     ix = [i for _ in range(R) for i in keep]
-    # fileId directory names: the upload's device-computed fileIds
     dig = fd[:R * 32].view(R, 32).cpu().numpy()
     tmp = tempfile.mkdtemp(prefix="dfs_store_")
     try:
         store = FragmentStore(1, tmp, engine=eng)
         refs = make_refs(off, ln, fi, ix)
-        # allocate the pinned staging ring outside the timed region (a 1-byte
-        # write of fragment 0 of file 0, truncated by the timed write)
-        store.write(dig, files.data_ptr(), make_refs([off[0]], [1], [0], [0]),
-                    device=True)
+        store.write(dig, files.data_ptr(), make_refs([off[0]], [1], [0], [0]), device=True)  # staging ring alloc
         t0 = time.perf_counter()
         st = store.write(dig, files.data_ptr(), refs, device=True)
         t_w = time.perf_counter() - t0
@@ -489,6 +437,8 @@ def store_leg(args, eng, files, fd, S, N, F, dev, log):
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     log(f"store: {2 * R} fragments, {total / 1e9:.2f} GB: write {t_w * 1e3:.0f} ms, read {t_r * 1e3:.0f} ms, ok={ok}")
+    if not ok:
+        raise LegError("store leg: status or bytes differ")
     return {"files": R, "fragments": 2 * R, "bytes": total, "node": 1,
             "write_ms": round(t_w * 1e3, 2), "write_gbs": round(total / t_w / 1e9, 2),
             "read_ms": round(t_r * 1e3, 2), "read_gbs": round(total / t_r / 1e9, 2), "ok": ok,
@@ -507,7 +457,7 @@ def long_leg(args):
     import torch
     import dfs_amd
     from dfs_amd.streaming import StreamingUpload, synth_fill_at
-    F, S, N, chunk = args.long_files, args.long_size, args.nfrag, args.long_chunk
+    F, S, N, chunk = args.long_files, args.long_size, 5, args.long_chunk
     dev = torch.device("cuda", 0)
     eng = dfs_amd.FragmentEngine(0)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
@@ -557,14 +507,282 @@ def long_leg(args):
            "wall_ms_incl_synth": round(wall * 1e3, 3), "verified": bool(ok)}
     print(json.dumps(res), flush=True)
     eng.close()
+    return 0 if ok else 3
 
 
+# ---------------------------------------------------------------------------
+# N > 1: upload + placement pipeline over RCCL
+# ---------------------------------------------------------------------------
+class Shard:
+    """This rank's files in `chunks` upload plans (fragment-major Base64, so
+    group f of a chunk is one span) with their Base64, held and digest
+    buffers; `table[c]` = every rank's group sizes of chunk c."""
+
+    def __init__(self, args, eng, comm, files, dev):
+        import numpy as np
+        import torch
+        import dfs_amd
+        from dfs_amd import placement as P
+        F, S, N = args.files, args.file_size, args.nfrag
+        C = max(1, min(args.chunks, F))
+        bounds = [F * c // C for c in range(C + 1)]
+        self.chunks = []
+        for c in range(C):
+            a, b = bounds[c], bounds[c + 1]
+            spans = np.stack([np.arange(a, b, dtype=np.uint64) * np.uint64(S),
+                              np.full(b - a, S, dtype=np.uint64)], axis=1)
+            plan = dfs_amd.UploadPlan(eng, spans, N, frag_major=True, align128=args.align128)
+            offs = plan.b64_offsets()
+            grp = [int(offs[f]) for f in range(N)] + [int(offs[-1])]
+            table = comm.sizes([grp[f + 1] - grp[f] for f in range(N)])
+            lay = P.held_layout(comm.world, comm.rank, N, table)
+            ch = {"a": a, "b": b, "plan": plan, "grp": grp, "table": table, "lay": lay,
+                  "b64": torch.empty(max(grp[-1], 1), dtype=torch.uint8, device=dev),
+                  "held": torch.empty(max(int(lay[N]), 1), dtype=torch.uint8, device=dev),
+                  "ev_up": torch.cuda.Event(), "ev_placed": torch.cuda.Event()}
+            for mode in ("ring", "star"):
+                ops, _, _ = P.plan(comm.world, comm.rank, N, table, mode)
+                ch["sent_" + mode] = P.bytes_sent(ops)
+            self.chunks.append(ch)
+        self.fd = torch.empty(F * 32, dtype=torch.uint8, device=dev)
+        self.frd = torch.empty(F * N * 32, dtype=torch.uint8, device=dev)
+        self.files, self.N = files, N
+
+    def upload(self, c, flags=0):
+        ch = self.chunks[c]
+        ch["plan"].run(self.files.data_ptr(), self.fd.data_ptr() + 32 * ch["a"],
+                       self.frd.data_ptr() + 32 * self.N * ch["a"], ch["b64"].data_ptr(), flags)
+
+
+def multi_gpu(args, world, rank, local, log):
+    """N > 1 step: upload (compute stream) + placement (comm stream), chunk c's
+    placement beside chunk c+1's hashing.  Returns (result dict, ok)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import dfs_amd
+    from dfs_amd import placement as P
+    from dfs_amd.engine import download_device
+    dev = torch.device("cuda", local)
+    F, S, N = args.files, args.file_size, args.nfrag
+    eng = dfs_amd.FragmentEngine(local)   # compute ctx
+    eng_c = dfs_amd.FragmentEngine(local)  # comm ctx (RCCL on its own stream)
+    s_comp, s_comm = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    eng.set_stream(s_comp.cuda_stream)
+    eng_c.set_stream(s_comm.cuda_stream)
+    uid = [P.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    comm = P.Comm(eng_c, uid[0], world, rank)
+    files = torch.empty(F * S + 64, dtype=torch.uint8, device=dev)
+    spans = np.stack([np.arange(F, dtype=np.uint64) * np.uint64(S), np.full(F, S, dtype=np.uint64)], axis=1)
+    dfs_amd.synth_fill(eng, files.data_ptr(), spans, rank * F, SEED)
+    sh = Shard(args, eng, comm, files, dev)
+    C = len(sh.chunks)
+    flags = dfs_amd.DFS_SERIAL if args.mode == "serial" else 0
+    torch.cuda.synchronize(dev)
+    log(f"{world} ranks x {F} files x {S} B, N={N}, {C} chunks, placement {args.placement}")
+
+    def step(mode, compute=True, place=True):
+        for c, ch in enumerate(sh.chunks):
+            if compute:
+                s_comp.wait_event(ch["ev_placed"])  # chunk c's Base64 is free again
+                sh.upload(c, flags)
+                ch["ev_up"].record(s_comp)
+            if place:
+                s_comm.wait_event(ch["ev_up"])
+                comm.place(mode, ch["table"], ch["b64"].data_ptr(), ch["held"].data_ptr())
+                ch["ev_placed"].record(s_comm)
+
+    def timed(fn, reps):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item()) / reps
+
+    for _ in range(args.warmup):
+        step(args.placement)
+    t_step = timed(lambda: step(args.placement), args.steps)
+    # the same step without the exchange, and each placement alone
+    t_comp = timed(lambda: step(args.placement, place=False), max(1, min(args.steps, 3)))
+    # SHA-256 kernel time per launch (one launch per chunk), HIP events on
+    # the compute stream, outside the timed steps
+    eng.set_profiling(True)
+    sha_ms = []
+    for c in range(C):
+        sh.upload(c, flags)
+        sha_ms.append(eng.timings()["sha"])
+    eng.set_profiling(False)
+    t_place = {}
+    for mode in ("star", "ring"):
+        step(mode, compute=False)
+        t_place[mode] = timed(lambda m=mode: step(m, compute=False), max(1, min(args.steps, 3)))
+    # held buffers after ring == after star: SHA-256 of every held group
+    # (the library's own kernel as a checksum of checksums)
+    def held_digests():
+        from dfs_amd.engine import sha256_device
+        out = []
+        for ch in sh.chunks:
+            n = int(ch["lay"][N])
+            piece = 1 << 20
+            sp = np.array([(o, min(piece, n - o)) for o in range(0, n, piece)], dtype=np.uint64)
+            out.append(sha256_device(eng_c, ch["held"].data_ptr(), sp).tobytes() if n else b"")
+        return out
+    torch.cuda.synchronize(dev)
+    dig_ring = held_digests()
+    step("star", compute=False)
+    torch.cuda.synchronize(dev)
+    ok = dig_ring == held_digests()
+    # Degraded read (BASELINE configs[4]): the last GPU offline; every other
+    # rank fetches its groups back from the live holders (SN:422-446), then
+    # Base64-decodes them into place with per-fragment and fileId verify.
+    offline = [world - 1]
+    fetch_ms = dl_ms = 0.0
+    dl_ok = True
+    out = torch.empty(max(sh.chunks[0]["b"] - sh.chunks[0]["a"], 1) * S, dtype=torch.uint8, device=dev)
+    back = torch.empty(max(ch["grp"][-1] for ch in sh.chunks), dtype=torch.uint8, device=dev)
+    for ch in sh.chunks:
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        st = comm.fetch(ch["table"], ch["held"].data_ptr(), back.data_ptr(), offline)
+        torch.cuda.synchronize(dev)
+        fetch_ms += (time.perf_counter() - t0) * 1e3
+        if rank in offline:
+            continue
+        nf = ch["b"] - ch["a"]
+        dl_ok &= bool((st == 0).all()) and bool(torch.equal(back[:ch["grp"][-1]], ch["b64"][:ch["grp"][-1]]))
+        t0 = time.perf_counter()
+        status = download_device(eng_c, back.data_ptr(), ch["plan"].b64_spans([S] * nf), nf, N,
+                                 np.full(nf, S, np.uint64), sh.frd.data_ptr() + 32 * N * ch["a"],
+                                 sh.fd.data_ptr() + 32 * ch["a"], out.data_ptr(),
+                                 np.arange(nf, dtype=np.uint64) * np.uint64(S))
+        dl_ms += (time.perf_counter() - t0) * 1e3
+        dl_ok &= bool((status == 0).all()) and bool(torch.equal(out[:nf * S], files[ch["a"] * S:ch["b"] * S]))
+    flag = torch.tensor([1 if (ok and dl_ok) else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    ok_all = bool(flag.item())
+    sent = {m: sum(ch["sent_" + m] for ch in sh.chunks) for m in ("ring", "star")}
+    sent_t = torch.tensor([sent["ring"], sent["star"]], dtype=torch.float64, device=dev)
+    dist.all_reduce(sent_t)
+    held_bytes = sum(int(ch["lay"][N]) for ch in sh.chunks)
+    res = {
+        "step_s": t_step,
+        "placement": {
+            "mode_in_step": args.placement, "chunks": C, "node_to_gpu": "node k on GPU k mod W",
+            "compute_only_ms": round(t_comp * 1e3, 3),
+            "compute_only_gbps": round(F * S * world / t_comp / 1e9, 3),
+            "star_ms": round(t_place["star"] * 1e3, 3),
+            "star_xgmi_gbps_per_gpu": round(sent_t[1].item() / world / t_place["star"] / 1e9, 2),
+            "ring_ms": round(t_place["ring"] * 1e3, 3),
+            "ring_xgmi_gbps_per_gpu": round(sent_t[0].item() / world / t_place["ring"] / 1e9, 2),
+            "bytes_sent_per_gpu": {"star": int(sent_t[1].item() / world), "ring": int(sent_t[0].item() / world)},
+            "held_bytes_per_gpu": held_bytes, "ring_equals_star": ok,
+            "degraded": {"offline_gpu": world - 1, "fetch_ms": round(fetch_ms, 3), "download_ms": round(dl_ms, 3),
+                         "download_gbps": round(F * S / (dl_ms / 1e3) / 1e9, 2) if dl_ms else None,
+                         "ok": ok_all},
+            "note": "xgmi_gbps = bytes this GPU sends / placement time (RCCL send/recv, dfs_place_ring / "
+                    "dfs_place_star); download = Base64 decode into place + fragment and fileId SHA-256 verify of "
+                    "the fetched groups (dfs_download_batch), wall clock"},
+        "sha_ms_per_launch": float(np.mean(sha_ms)), "files_per_launch": F / C, "ok": ok_all}
+    for ch in sh.chunks:
+        ch["plan"].close()
+    comm.close()
+    eng.close()
+    eng_c.close()
+    return res, ok_all
+
+
+def roofline_n(res, S, N):
+    """SHA-256 kernel roofline at N > 1 (rank 0's compute ctx, one launch per
+    chunk of files_per_launch files)."""
+    blocks = res["files_per_launch"] * (sha_blocks(S) + sum(sha_blocks(x) for x in split(S, N)))
+    ms = res["sha_ms_per_launch"]
+    tops = blocks * OPS_PER_BLOCK_CANON / (ms / 1e3) / 1e12
+    return {"bound": "valu", "achieved": round(tops, 3), "peak": round(VALU_PEAK_TOPS, 3), "unit": "Tops/s (int32)",
+            "frac": round(tops / VALU_PEAK_TOPS, 4), "traffic": None, "kernel": "sha256_lanes", "ms": round(ms, 3),
+            "blocks_per_launch": int(blocks), "ops_per_block": OPS_PER_BLOCK_CANON,
+            "note": "compute-only launches (no placement beside them), rank 0"}
+
+
+def dry_run(args, world, rank, log):
+    """Harness check on CPU (gloo): rendezvous, barrier + max-over-ranks
+    timing and the placement schedules executed over gloo point-to-point on
+    synthetic byte groups.  Never a measurement (no GPU kernels run)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from dfs_amd import placement as P
+    N = args.nfrag
+    rng = np.random.default_rng(rank)
+    sizes = [int(x) for x in rng.integers(1000, 5000, N)]
+    src = torch.from_numpy(rng.integers(0, 256, sum(sizes), dtype=np.uint8))
+    t = torch.tensor(sizes, dtype=torch.int64)
+    rows = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(rows, t)
+    table = np.stack([r.numpy() for r in rows]).astype(np.uint64)
+    ops, lay, _ = P.plan(world, rank, N, table, args.placement)
+    held = torch.zeros(int(lay[N]), dtype=torch.uint8)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        P.run_plan_torch(ops, src, held)
+    dist.barrier()
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    fops, flay, fst = P.plan(world, rank, N, table, "fetch", [world - 1])
+    back = torch.zeros(int(flay[N]), dtype=torch.uint8)
+    P.run_plan_torch(fops, held, back)
+    ok = rank == world - 1 or bool(torch.equal(back, src))
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return float(tt.item()) / max(args.steps, 1), bool(flag.item()), int(table.sum())
+
+
+# ---------------------------------------------------------------------------
 def main():
     args = parse()
-    if args.config == 4:
-        return long_leg(args)
     if args.serial:
         args.mode = "serial"
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    resolve_config(args, world)
+    if args.config == 4:
+        return long_leg(args)
+
+    def log(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    if args.dry_run:
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group("gloo", rank=0, world_size=1)
+        per, ok, nbytes = dry_run(args, world, rank, log)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                              "warmup": args.warmup, "ms_per_step": round(per * 1e3, 3), "higher_is_better": True,
+                              "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "dry-run",
+                              "dry_run": True, "placed_bytes": nbytes, "verified": ok,
+                              "config": {"workload": "harness check (gloo, CPU tensors), no GPU work"}}), flush=True)
+        dist.destroy_process_group()
+        return 0 if ok else 3
+
     # read by dfs_open: two-kernel mode vs the fused SHA+Base64 kernel
     os.environ["DFS_UPLOAD_MODE"] = "kernels" if args.mode != "fused" else "fused"
     import numpy as np
@@ -572,31 +790,46 @@ def main():
     import torch.distributed as dist
     import dfs_amd
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        # A stuck exchange in the side legs must raise (and be reported in the
-        # JSON line) rather than hang or abort the job: blocking waits with a
-        # bounded timeout, communicator cleanup without process teardown.
-        os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
-        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
         import datetime
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local),
-                                timeout=datetime.timedelta(seconds=240))
-    dev = torch.device("cuda", local if world > 1 else 0)
-
-    def log(msg):
+                                timeout=datetime.timedelta(seconds=600))
+        S, N, F = args.file_size, args.nfrag, args.files
+        failures = []
+        try:
+            res, ok = multi_gpu(args, world, rank, local, log)
+        except Exception as e:  # report, then fail the run
+            import traceback
+            traceback.print_exc()
+            res, ok = {"step_s": float("nan"), "placement": {"error": repr(e)[:300]}}, False
+            failures.append("placement")
+        elapsed = res["step_s"]
+        value = F * S * world / elapsed / 1e9 if elapsed == elapsed else None
         if rank == 0:
-            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+            print(json.dumps({
+                "metric": METRIC, "value": round(value, 3) if value else None, "unit": "GB/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(elapsed * 1e3, 3) if value else None, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+                "data": "synthetic (splitmix64, seed 0x5EED5EED), resident in HBM",
+                "config": {"workload": f"upload + placement: {F} files x {S} B per GPU (BASELINE configs[2] shard), "
+                                       f"N={N} fragments: fileId SHA-256 + fragment SHA-256 + fragment Base64, "
+                                       f"then {args.placement} placement of the Base64 over RCCL/xGMI",
+                           "files_per_gpu": F, "file_bytes": S, "nfrag": N, "parallelism": f"files sharded x{world}",
+                           "placement": args.placement},
+                "roofline": roofline_n(res, S, N) if ok else None,
+                "placement": res["placement"], "verified": ok}), flush=True)
+        dist.destroy_process_group()
+        return 0 if ok and not failures else 3
 
+    # ---------------- N = 1 ----------------
+    dev = torch.device("cuda", 0)
     S, N, F = args.file_size, args.nfrag, args.files
-    eng = dfs_amd.FragmentEngine(dev.index)
+    eng = dfs_amd.FragmentEngine(0)
     spans = np.stack([np.arange(F, dtype=np.uint64) * np.uint64(S), np.full(F, S, dtype=np.uint64)], axis=1)
-    first_file = rank * F  # this rank's shard of the global file set
     files = torch.empty(F * S + 64, dtype=torch.uint8, device=dev)
-    dfs_amd.synth_fill(eng, files.data_ptr(), spans, first_file, SEED)
+    dfs_amd.synth_fill(eng, files.data_ptr(), spans, 0, SEED)
     plan = dfs_amd.UploadPlan(eng, spans, N, align128=args.align128)
     fd = torch.empty(F * 32, dtype=torch.uint8, device=dev)
     frd = torch.empty(F * N * 32, dtype=torch.uint8, device=dev)
@@ -605,7 +838,7 @@ def main():
     eng.set_stream(stream.cuda_stream)
     flags = dfs_amd.DFS_SERIAL if args.mode == "serial" else 0
     torch.cuda.synchronize(dev)
-    log(f"rank0: {F} files x {S} B, N={N}, b64 {plan.b64_total / 1e9:.2f} GB, world {world}")
+    log(f"{F} files x {S} B, N={N}, b64 {plan.b64_total / 1e9:.2f} GB")
 
     for _ in range(args.warmup):
         plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), flags)
@@ -614,8 +847,6 @@ def main():
     # ---- timed region ---------------------------------------------------------
     eng.set_profiling(True)
     sha_ms = []
-    if world > 1:
-        dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -623,17 +854,10 @@ def main():
         t = eng.timings()  # waits on this step's last HIP event; per-kernel ms
         sha_ms.append(t["sha"])
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
 
-    # ---- fragment-only variant: the same step without the fileId
-    # SHA-256 (SN:127), e.g. for a caller that already knows the content address.
+    # ---- fragment-only variant: no fileId SHA-256 (SN:127)
     frag_only = None
     if args.frag_only_steps:
         eng.set_profiling(True)
@@ -647,10 +871,9 @@ def main():
         frag_only = {"ms_per_step": round(fo, 3), "gbps": round(F * S / (fo / 1e3) / 1e9, 3),
                      "sha_ms": round(float(np.mean(fo_sha)), 3),
                      "note": "fragment SHA-256 + Base64 only (no fileId SHA-256), HIP-event device time, this GPU"}
+        plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), flags)  # restore fileIds
 
     # ---- the HBM-bound Base64 encode pass alone (roofline_b64) -----------------
-    # Outside the timed steps (in the default fused mode the upload writes the
-    # Base64 from the SHA kernel); same plan, same buffers, own HIP events.
     eng.set_profiling(True)
     b64_ms = []
     for _ in range(max(1, args.b64_steps)):
@@ -661,7 +884,7 @@ def main():
 
     # ---- spot-check against the oracle (outside the timed region) -------------
     ok = True
-    if rank == 0 and args.verify:
+    if args.verify:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # checker only
         idx = sorted(set([0, F - 1] + list(np.random.default_rng(1).integers(0, F, args.verify))))
@@ -669,7 +892,7 @@ def main():
         fdh = fd.view(F, 32).cpu().numpy()
         frdh = frd.view(F, N, 32).cpu().numpy()
         for f in idx:
-            data = O.c_synth(first_file + f, 0, S)
+            data = O.c_synth(f, 0, S)
             efd, efrd, eb64, eoff = O.c_upload_batch([data], N)
             k0 = f * N
             got_b64 = b"".join(b64[int(o):int(o + n)].cpu().numpy().tobytes() for o, n in bsp[k0:k0 + N])
@@ -678,8 +901,7 @@ def main():
         log(f"oracle spot-check of {len(idx)} files: {'OK' if ok else 'MISMATCH'}")
 
     # ---- numbers -----------------------------------------------------------------
-    total_bytes = F * S * world * args.steps  # file bytes all ranks pushed through the timed steps
-    value = total_bytes / elapsed / 1e9
+    value = F * S * args.steps / elapsed / 1e9
     lens = split(S, N)
     blocks = F * (sha_blocks(S) + sum(sha_blocks(x) for x in lens))
     sha_avg = float(np.mean(sha_ms)) / 1e3
@@ -688,27 +910,21 @@ def main():
     issued_tops = blocks * OPS_PER_BLOCK_ISSUED / sha_avg / 1e12
     b64_bytes = F * S + 4 * F * sum((x + 2) // 3 for x in lens)  # read + Base64 written
     b64_gbs = b64_bytes / b64_avg / 1e9
-    traffic = None
+    traffic, traffic_src = None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             if pmc.get("workload") == f"{F}x{S}/N{N}":
                 traffic = pmc.get("sha_hbm_bytes_per_launch")
+                traffic_src = ("profiles/pmc_summary.json: rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this bench "
+                               "command (a separate profiled run, not this one)")
         except Exception:
             traffic = None
     result = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u32",
+        "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (splitmix64, seed 0x5EED5EED), resident in HBM",
         "config": {"workload": f"upload: {F} files x {S} B per GPU, N={N} fragments: fileId SHA-256 + "
                                f"fragment SHA-256 + fragment Base64",
@@ -719,9 +935,9 @@ def main():
                    "b64_layout": "128-byte aligned fragment starts" if args.align128 else "packed"},
         "roofline": {"bound": "valu", "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 3),
                      "unit": "Tops/s (int32)", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
-                     "traffic": traffic, "kernel": "sha256_lanes" + (" (+ fused Base64)" if args.mode == "fused" else ""),
-                     "ms": round(sha_avg * 1e3, 3),
-                     "blocks_per_launch": blocks, "ops_per_block": OPS_PER_BLOCK_CANON,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "sha256_lanes" + (" (+ fused Base64)" if args.mode == "fused" else ""),
+                     "ms": round(sha_avg * 1e3, 3), "blocks_per_launch": blocks, "ops_per_block": OPS_PER_BLOCK_CANON,
                      "valu_issue_frac": round(issued_tops / VALU_PEAK_TOPS, 4)},
         "roofline_b64": {"bound": "hbm", "achieved": round(b64_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(b64_gbs / HBM_PEAK_GBS, 4), "kernel": "b64_encode_kernel",
@@ -732,40 +948,31 @@ def main():
     }
     if frag_only:
         result["fragment_only"] = frag_only
+    failures = [] if ok else ["verify"]
+    legs = []
     if not args.no_download:
-        try:
-            result["download"] = download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log)
-        except Exception as e:
-            result["download"] = {"error": repr(e)[:300]}
+        legs.append(("download", lambda: download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log)))
     if not args.no_wire:
-        try:
-            result["wire"] = wire_leg(args, eng, files, fd, frd, S, N, F, dev, log)
-        except Exception as e:
-            result["wire"] = {"error": repr(e)[:300]}
+        legs.append(("wire", lambda: wire_leg(args, eng, files, fd, frd, S, N, F, dev, log)))
     if not args.no_store:
+        legs.append(("store", lambda: store_leg(args, eng, files, fd, S, N, F, dev, log)))
+    if not args.no_cpu_baseline:
+        legs.append(("cpu_baseline", lambda: cpu_baseline(args, log)))
+    for name, fn in legs:
         try:
-            result["store"] = store_leg(args, eng, files, fd, S, N, F, dev, log)
-        except Exception as e:
-            result["store"] = {"error": repr(e)[:300]}
-    if world > 1 and not args.no_replicate:
-        # The upload's Base64 (91.6 GB at config 2) is not needed any more: free
-        # it so the placement buffers (held groups of every rank, all-to-all
-        # send / receive copies) fit beside the files in HBM.
-        b64 = None
-        torch.cuda.empty_cache()
-        try:
-            result["replication"] = replication_leg(args, eng, files, S, N, dev, log)
-        except Exception as e:  # never lose the main line to the side measurement
-            result["replication"] = {"error": repr(e)[:300]}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, log)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+            result[name] = fn()
+        except Exception as e:  # the line is still printed; the exit code reports the failure
+            import traceback
+            traceback.print_exc()
+            result[name] = {"error": repr(e)[:300]}
+            failures.append(name)
+    if failures:
+        result["failed_legs"] = failures
+    print(json.dumps(result), flush=True)
     plan.close()
     eng.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return 3 if failures else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

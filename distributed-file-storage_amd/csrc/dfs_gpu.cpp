@@ -259,6 +259,7 @@ const char* dfs_strerror(int code) {
         case DFS_E_NODEV: return "no gfx950 (MI355X) device available";
         case DFS_E_WIRE: return "storeFragments body not in buildFragmentsJson form (parse it with parseJson)";
         case DFS_E_IO: return "fragment store I/O error (IOException)";
+        case DFS_E_COMM: return dfs_comm_last_error();
         default: return "unknown error";
     }
 }

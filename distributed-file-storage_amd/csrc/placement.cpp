@@ -1,0 +1,430 @@
+// placement.cpp — replica placement and degraded fetch across GPUs over RCCL
+// (include/dfs_gpu.h, dfs_comm_* / dfs_place_*).
+//
+// Reference (StorageNode.java, SN:line): node k (0-based) stores fragments
+// {k, (k+1) mod N} (:143-145, :199-200); the uploader sends every peer its
+// pair (star fan-out, :195-224; the receiver checks the hashes, :248-257);
+// a download takes fragment i locally, else from node i, else from node i-1
+// (:422-440), and fails with "Could not retrieve fragment i" (:443-446).
+//
+// MI355X mapping: one rank per GPU, node k hosted by rank
+// k mod W.  A rank's Base64 is fragment-major: group f = the Base64 of
+// fragment f of every file the rank uploaded, groups back to back.  After a
+// placement every rank holds, for each fragment f it hosts, "held group f" =
+// group f of rank 0, rank 1, ... concatenated in rank order.
+//
+//   RING  primary scatter (group f -> the rank of node f) then the replica
+//         step (that rank forwards held group f to the rank of node f-1):
+//         with W == N the ring g -> g-1 of north_star, one xGMI link per GPU
+//         (BASELINE "GPU g sends to g+1" under the relabel node k <-> GPU k+1).
+//   STAR  the reference's own fan-out as one all-to-all: group f goes
+//         straight from its uploader to both holders, every link busy.
+//   FETCH degraded read: every live rank gets its own groups back from the
+//         first live holder in SN:427-428 order.
+//
+// The transfer schedule is a pure host function (dfs_place_plan), so it is
+// checked on the CPU by simulating every rank in one process
+// (tests/test_placement_plan.py); the runner only issues its ops:
+// ncclSend / ncclRecv inside ncclGroupStart / End per phase, local copies as
+// device-to-device hipMemcpyAsync, all on the ctx stream.  Between a pair of
+// ranks sends and receives are issued in the same order on both sides, which
+// is how RCCL matches them.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/dfs_gpu.h"
+#include "dfs_internal.h"
+
+static_assert(DFS_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
+
+struct dfs_comm {
+    dfs_ctx* ctx = nullptr;
+    ncclComm_t nc = nullptr;
+    uint32_t nranks = 0, rank = 0;
+    uint64_t* d_sizes = nullptr;  // all-gather scratch (nranks * kMaxFrag words)
+};
+
+namespace {
+
+constexpr uint32_t kMaxFrag = 64;
+constexpr uint32_t kMaxRanks = 64;  // offline masks are 64-bit
+
+thread_local char g_last_comm[160];
+
+int comm_fail(ncclResult_t r, const char* what) {
+    std::snprintf(g_last_comm, sizeof g_last_comm, "%s: %s", what, ncclGetErrorString(r));
+    return DFS_E_COMM;
+}
+
+#define NCCLC(x)                                        \
+    do {                                                \
+        ncclResult_t r_ = (x);                          \
+        if (r_ != ncclSuccess) return comm_fail(r_, #x); \
+    } while (0)
+#define HIPCHK(x)                                       \
+    do {                                                \
+        if ((x) != hipSuccess) return DFS_E_HIP;        \
+    } while (0)
+
+uint32_t holder_a(uint32_t f, uint32_t N, uint32_t W) { return f % W; }                  // node f (SN:427)
+uint32_t holder_b(uint32_t f, uint32_t N, uint32_t W) { return ((f + N - 1) % N) % W; }  // node f-1 (SN:428)
+bool holds(uint32_t g, uint32_t f, uint32_t N, uint32_t W) { return holder_a(f, N, W) == g || holder_b(f, N, W) == g; }
+
+struct Plan {
+    std::vector<dfs_xfer> ops;
+    std::vector<uint64_t> dst_off;  // nfrag + 1
+    std::vector<int32_t> status;    // nfrag
+    uint32_t phases = 0;
+};
+
+// Bytes of rank r's group f.
+inline uint64_t T(const uint64_t* table, uint32_t N, uint32_t r, uint32_t f) { return table[static_cast<uint64_t>(r) * N + f]; }
+
+void add(Plan& p, uint32_t phase, uint32_t kind, int32_t peer, uint32_t f, uint32_t from_dst, uint64_t src, uint64_t dst,
+         uint64_t len) {
+    if (!len) return;  // both sides skip empty transfers (they see the same table)
+    dfs_xfer x{};
+    x.phase = phase;
+    x.kind = kind;
+    x.peer = peer;
+    x.frag = f;
+    x.from_dst = from_dst;
+    x.src_off = src;
+    x.dst_off = dst;
+    x.len = len;
+    p.ops.push_back(x);
+}
+
+int build_plan(uint32_t W, uint32_t me, uint32_t N, const uint64_t* table, uint32_t mode, uint64_t offline, Plan& p) {
+    if (!W || W > kMaxRanks || me >= W || !N || N > kMaxFrag || !table) return DFS_E_ARG;
+    if (mode > DFS_PLACE_FETCH) return DFS_E_ARG;
+    p.ops.clear();
+    p.dst_off.assign(N + 1, 0);
+    p.status.assign(N, DFS_OK);
+    // own group offsets in the fragment-major source (groups back to back)
+    std::vector<uint64_t> goff(N + 1, 0);
+    for (uint32_t f = 0; f < N; ++f) goff[f + 1] = goff[f] + T(table, N, me, f);
+    // position of rank r's piece inside held group f
+    auto piece = [&](uint32_t f, uint32_t r) {
+        uint64_t o = 0;
+        for (uint32_t q = 0; q < r; ++q) o += T(table, N, q, f);
+        return o;
+    };
+    auto total = [&](uint32_t f) { return piece(f, W); };
+    if (mode == DFS_PLACE_FETCH) {
+        for (uint32_t f = 0; f <= N; ++f) p.dst_off[f] = goff[f];  // same layout as the source groups
+    } else {
+        uint64_t o = 0;
+        for (uint32_t f = 0; f < N; ++f) {
+            if (holds(me, f, N, W)) {
+                p.dst_off[f] = o;
+                o += total(f);
+            } else {
+                p.dst_off[f] = UINT64_MAX;
+            }
+        }
+        p.dst_off[N] = o;
+    }
+    const uint64_t* H = p.dst_off.data();
+    if (mode == DFS_PLACE_RING) {
+        p.phases = 2;
+        // phase 0: primary scatter, group f -> rank of node f
+        for (uint32_t f = 0; f < N; ++f) {
+            const uint32_t a = holder_a(f, N, W);
+            if (a == me) {
+                for (uint32_t r = 0; r < W; ++r) {
+                    if (r == me) add(p, 0, DFS_XFER_COPY, -1, f, 0, goff[f], H[f] + piece(f, r), T(table, N, r, f));
+                    else add(p, 0, DFS_XFER_RECV, static_cast<int32_t>(r), f, 0, 0, H[f] + piece(f, r), T(table, N, r, f));
+                }
+            } else {
+                add(p, 0, DFS_XFER_SEND, static_cast<int32_t>(a), f, 0, goff[f], 0, T(table, N, me, f));
+            }
+        }
+        // phase 1: replica step, rank of node f -> rank of node f-1
+        for (uint32_t f = 0; f < N; ++f) {
+            const uint32_t a = holder_a(f, N, W), b = holder_b(f, N, W);
+            if (a == b) continue;
+            if (me == a) add(p, 1, DFS_XFER_SEND, static_cast<int32_t>(b), f, 1, H[f], 0, total(f));
+            else if (me == b) add(p, 1, DFS_XFER_RECV, static_cast<int32_t>(a), f, 0, 0, H[f], total(f));
+        }
+    } else if (mode == DFS_PLACE_STAR) {
+        p.phases = 1;
+        for (uint32_t g = 0; g < W; ++g)
+            for (uint32_t f = 0; f < N; ++f) {
+                if (!holds(g, f, N, W)) continue;
+                if (g == me) add(p, 0, DFS_XFER_COPY, -1, f, 0, goff[f], H[f] + piece(f, me), T(table, N, me, f));
+                else add(p, 0, DFS_XFER_SEND, static_cast<int32_t>(g), f, 0, goff[f], 0, T(table, N, me, f));
+            }
+        for (uint32_t f = 0; f < N; ++f) {
+            if (!holds(me, f, N, W)) continue;
+            for (uint32_t r = 0; r < W; ++r)
+                if (r != me) add(p, 0, DFS_XFER_RECV, static_cast<int32_t>(r), f, 0, 0, H[f] + piece(f, r), T(table, N, r, f));
+        }
+    } else {  // FETCH
+        p.phases = 1;
+        auto off = [&](uint32_t g) { return (offline >> g) & 1u; };
+        // every rank walks every requester's plan so both sides of each
+        // transfer are issued in the same order
+        for (uint32_t q = 0; q < W; ++q) {
+            if (off(q)) continue;
+            for (uint32_t f = 0; f < N; ++f) {
+                int32_t s = -1;
+                if (holds(q, f, N, W)) s = static_cast<int32_t>(q);  // tryLoadFragmentLocal, SN:423
+                else if (!off(holder_a(f, N, W))) s = static_cast<int32_t>(holder_a(f, N, W));  // nodeA, SN:427
+                else if (!off(holder_b(f, N, W))) s = static_cast<int32_t>(holder_b(f, N, W));  // nodeB, SN:428
+                if (s < 0) {
+                    if (q == me) p.status[f] = DFS_E_MISSING;  // SN:443-446
+                    continue;
+                }
+                const uint64_t len = T(table, N, q, f);
+                if (static_cast<uint32_t>(s) == me) {
+                    // serve q's piece of my held group f (dst_off of the server's layout)
+                    uint64_t ho = 0;
+                    for (uint32_t h = 0; h < f; ++h)
+                        if (holds(me, h, N, W)) ho += total(h);
+                    if (q == me) add(p, 0, DFS_XFER_COPY, -1, f, 0, ho + piece(f, q), H[f], len);
+                    else add(p, 0, DFS_XFER_SEND, static_cast<int32_t>(q), f, 0, ho + piece(f, q), 0, len);
+                } else if (q == me) {
+                    add(p, 0, DFS_XFER_RECV, s, f, 0, 0, H[f], len);
+                }
+            }
+        }
+        if (offline >> me & 1u)  // an offline rank neither serves nor requests
+            for (uint32_t f = 0; f < N; ++f) p.status[f] = DFS_E_MISSING;
+    }
+    return DFS_OK;
+}
+
+// Issue one plan per comm (ncomms > 1: one process driving several GPUs,
+// every comm's ops inside the same group per phase).
+int run_plans(dfs_comm* const* comms, uint32_t ncomms, const std::vector<Plan>& plans, const void* const* src,
+              void* const* dst) {
+    uint32_t phases = 0;
+    for (const Plan& p : plans) phases = p.phases > phases ? p.phases : phases;
+    for (uint32_t ph = 0; ph < phases; ++ph) {
+        // local copies first (same stream as the group: ordered before it)
+        for (uint32_t i = 0; i < ncomms; ++i) {
+            HIPCHK(hipSetDevice(dfs::ctx_device(comms[i]->ctx)));
+            hipStream_t s = dfs::ctx_stream(comms[i]->ctx);
+            for (const dfs_xfer& x : plans[i].ops) {
+                if (x.phase != ph || x.kind != DFS_XFER_COPY) continue;
+                const char* from = x.from_dst ? static_cast<const char*>(dst[i]) : static_cast<const char*>(src[i]);
+                HIPCHK(hipMemcpyAsync(static_cast<char*>(dst[i]) + x.dst_off, from + x.src_off, x.len,
+                                      hipMemcpyDeviceToDevice, s));
+            }
+        }
+        bool any = false;
+        for (uint32_t i = 0; i < ncomms && !any; ++i)
+            for (const dfs_xfer& x : plans[i].ops)
+                if (x.phase == ph && x.kind != DFS_XFER_COPY) {
+                    any = true;
+                    break;
+                }
+        if (!any) continue;
+        NCCLC(ncclGroupStart());
+        for (uint32_t i = 0; i < ncomms; ++i) {
+            if (ncomms > 1 && hipSetDevice(dfs::ctx_device(comms[i]->ctx)) != hipSuccess) {
+                (void)ncclGroupEnd();
+                return DFS_E_HIP;
+            }
+            hipStream_t s = dfs::ctx_stream(comms[i]->ctx);
+            for (const dfs_xfer& x : plans[i].ops) {
+                if (x.phase != ph || x.kind == DFS_XFER_COPY) continue;
+                ncclResult_t r;
+                if (x.kind == DFS_XFER_SEND) {
+                    const char* from = x.from_dst ? static_cast<const char*>(dst[i]) : static_cast<const char*>(src[i]);
+                    r = ncclSend(from + x.src_off, x.len, ncclUint8, x.peer, comms[i]->nc, s);
+                } else {
+                    r = ncclRecv(static_cast<char*>(dst[i]) + x.dst_off, x.len, ncclUint8, x.peer, comms[i]->nc, s);
+                }
+                if (r != ncclSuccess) {
+                    (void)ncclGroupEnd();
+                    return comm_fail(r, x.kind == DFS_XFER_SEND ? "ncclSend" : "ncclRecv");
+                }
+            }
+        }
+        NCCLC(ncclGroupEnd());
+    }
+    return DFS_OK;
+}
+
+int check_comms(dfs_comm* const* comms, uint32_t ncomms) {
+    if (!comms || !ncomms) return DFS_E_ARG;
+    for (uint32_t i = 0; i < ncomms; ++i)
+        if (!comms[i] || !comms[i]->nc || comms[i]->nranks != comms[0]->nranks) return DFS_E_ARG;
+    return DFS_OK;
+}
+
+int place(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table, uint32_t mode,
+          uint64_t offline, const void* const* src, void* const* dst, int32_t* frag_status) {
+    if (int rc = check_comms(comms, ncomms)) return rc;
+    if (!src || !dst) return DFS_E_ARG;
+    std::vector<Plan> plans(ncomms);
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        if (int rc = build_plan(comms[i]->nranks, comms[i]->rank, nfrag, table, mode, offline, plans[i])) return rc;
+        if (plans[i].dst_off[nfrag] && !dst[i]) return DFS_E_ARG;
+        for (const dfs_xfer& x : plans[i].ops)
+            if (x.kind != DFS_XFER_RECV && !x.from_dst && !src[i]) return DFS_E_ARG;
+        if (frag_status) std::memcpy(frag_status + static_cast<uint64_t>(i) * nfrag, plans[i].status.data(), 4ull * nfrag);
+    }
+    return run_plans(comms, ncomms, plans, src, dst);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dfs_comm_last_error(void) { return g_last_comm[0] ? g_last_comm : "RCCL error"; }
+
+int dfs_place_plan(uint32_t nranks, uint32_t rank, uint32_t nfrag, const uint64_t* table, uint32_t mode,
+                   uint64_t offline_mask, dfs_xfer* ops, uint32_t* nops, uint64_t* dst_off, int32_t* frag_status) {
+    if (!nops) return DFS_E_ARG;
+    Plan p;
+    if (int rc = build_plan(nranks, rank, nfrag, table, mode, offline_mask, p)) return rc;
+    const uint32_t cap = *nops;
+    *nops = static_cast<uint32_t>(p.ops.size());
+    if (dst_off) std::memcpy(dst_off, p.dst_off.data(), 8ull * (nfrag + 1));
+    if (frag_status) std::memcpy(frag_status, p.status.data(), 4ull * nfrag);
+    if (ops) {
+        if (cap < p.ops.size()) return DFS_E_ARG;
+        std::memcpy(ops, p.ops.data(), sizeof(dfs_xfer) * p.ops.size());
+    }
+    return DFS_OK;
+}
+
+int dfs_comm_unique_id(uint8_t* id) {
+    if (!id) return DFS_E_ARG;
+    ncclUniqueId u;
+    NCCLC(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return DFS_OK;
+}
+
+int dfs_comm_init_rank(dfs_ctx* ctx, const uint8_t* id, uint32_t nranks, uint32_t rank, dfs_comm** out) {
+    if (!ctx || !id || !out || !nranks || nranks > kMaxRanks || rank >= nranks) return DFS_E_ARG;
+    *out = nullptr;
+    HIPCHK(hipSetDevice(dfs::ctx_device(ctx)));
+    auto* c = new (std::nothrow) dfs_comm;
+    if (!c) return DFS_E_NOMEM;
+    c->ctx = ctx;
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&c->nc, static_cast<int>(nranks), u, static_cast<int>(rank));
+    if (r != ncclSuccess) {
+        delete c;
+        return comm_fail(r, "ncclCommInitRank");
+    }
+    *out = c;
+    return DFS_OK;
+}
+
+int dfs_comm_init_all(dfs_ctx* const* ctxs, uint32_t n, dfs_comm** out) {
+    if (!ctxs || !out || !n || n > kMaxRanks) return DFS_E_ARG;
+    std::vector<int> dev(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!ctxs[i]) return DFS_E_ARG;
+        dev[i] = dfs::ctx_device(ctxs[i]);
+        out[i] = nullptr;
+    }
+    std::vector<ncclComm_t> nc(n);
+    NCCLC(ncclCommInitAll(nc.data(), static_cast<int>(n), dev.data()));
+    for (uint32_t i = 0; i < n; ++i) {
+        auto* c = new (std::nothrow) dfs_comm;
+        if (!c) {
+            for (uint32_t j = 0; j < n; ++j) {
+                if (j < i) dfs_comm_destroy(out[j]);
+                else (void)ncclCommDestroy(nc[j]);
+                out[j] = nullptr;
+            }
+            return DFS_E_NOMEM;
+        }
+        c->ctx = ctxs[i];
+        c->nc = nc[i];
+        c->nranks = n;
+        c->rank = i;
+        out[i] = c;
+    }
+    return DFS_OK;
+}
+
+int dfs_comm_destroy(dfs_comm* c) {
+    if (!c) return DFS_E_ARG;
+    (void)hipSetDevice(dfs::ctx_device(c->ctx));
+    (void)hipStreamSynchronize(dfs::ctx_stream(c->ctx));
+    if (c->nc) (void)ncclCommDestroy(c->nc);
+    if (c->d_sizes) (void)hipFree(c->d_sizes);
+    delete c;
+    return DFS_OK;
+}
+
+int dfs_comm_info(const dfs_comm* c, uint32_t* nranks, uint32_t* rank) {
+    if (!c) return DFS_E_ARG;
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    return DFS_OK;
+}
+
+int dfs_place_sizes(dfs_comm* const* comms, uint32_t ncomms, const uint64_t* grp_len, uint32_t nfrag,
+                    uint64_t* table) {
+    if (int rc = check_comms(comms, ncomms)) return rc;
+    if (!grp_len || !table || !nfrag || nfrag > kMaxFrag) return DFS_E_ARG;
+    const uint32_t W = comms[0]->nranks;
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        dfs_comm* c = comms[i];
+        HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
+        if (!c->d_sizes) HIPCHK(hipMalloc(&c->d_sizes, 8ull * (W + 1) * kMaxFrag));
+        HIPCHK(hipMemcpyAsync(c->d_sizes + static_cast<uint64_t>(W) * kMaxFrag, grp_len + static_cast<uint64_t>(i) * nfrag,
+                              8ull * nfrag, hipMemcpyHostToDevice, dfs::ctx_stream(c->ctx)));
+    }
+    NCCLC(ncclGroupStart());
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        dfs_comm* c = comms[i];
+        if (ncomms > 1 && hipSetDevice(dfs::ctx_device(c->ctx)) != hipSuccess) {
+            (void)ncclGroupEnd();
+            return DFS_E_HIP;
+        }
+        ncclResult_t r = ncclAllGather(c->d_sizes + static_cast<uint64_t>(W) * kMaxFrag, c->d_sizes, nfrag, ncclUint64,
+                                       c->nc, dfs::ctx_stream(c->ctx));
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return comm_fail(r, "ncclAllGather");
+        }
+    }
+    NCCLC(ncclGroupEnd());
+    // every comm gathers the same table: read it back from the first
+    dfs_comm* c = comms[0];
+    HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
+    HIPCHK(hipMemcpyAsync(table, c->d_sizes, 8ull * W * nfrag, hipMemcpyDeviceToHost, dfs::ctx_stream(c->ctx)));
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        HIPCHK(hipSetDevice(dfs::ctx_device(comms[i]->ctx)));
+        HIPCHK(hipStreamSynchronize(dfs::ctx_stream(comms[i]->ctx)));
+    }
+    return DFS_OK;
+}
+
+int dfs_place_ring(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table,
+                   const char* const* d_b64, char* const* d_held) {
+    return place(comms, ncomms, nfrag, table, DFS_PLACE_RING, 0, reinterpret_cast<const void* const*>(d_b64),
+                 reinterpret_cast<void* const*>(d_held), nullptr);
+}
+
+int dfs_place_star(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table,
+                   const char* const* d_b64, char* const* d_held) {
+    return place(comms, ncomms, nfrag, table, DFS_PLACE_STAR, 0, reinterpret_cast<const void* const*>(d_b64),
+                 reinterpret_cast<void* const*>(d_held), nullptr);
+}
+
+int dfs_fetch_degraded(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table,
+                       uint64_t offline_mask, const char* const* d_held, char* const* d_out, int32_t* frag_status) {
+    return place(comms, ncomms, nfrag, table, DFS_PLACE_FETCH, offline_mask,
+                 reinterpret_cast<const void* const*>(d_held), reinterpret_cast<void* const*>(d_out), frag_status);
+}
+
+}  // extern "C"

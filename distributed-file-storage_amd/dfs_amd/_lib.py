@@ -27,6 +27,7 @@ DFS_E_FRAG_MISMATCH = -7
 DFS_E_NODEV = -8
 DFS_E_WIRE = -9
 DFS_E_IO = -10
+DFS_E_COMM = -11
 
 DFS_DEVICE_PTRS = 0x1
 DFS_NO_FILEID = 0x2
@@ -40,6 +41,10 @@ DFS_SHA_FINAL = 0x40
 
 DFS_SPAN_MISSING = (1 << 64) - 1
 
+DFS_COMM_ID_BYTES = 128
+DFS_PLACE_RING, DFS_PLACE_STAR, DFS_PLACE_FETCH = 0, 1, 2
+DFS_XFER_SEND, DFS_XFER_RECV, DFS_XFER_COPY = 0, 1, 2
+
 DFS_T_SHA, DFS_T_B64ENC, DFS_T_B64DEC, DFS_T_GATHER, DFS_T_TOTAL, DFS_T_COUNT = range(6)
 
 
@@ -49,6 +54,9 @@ class dfs_span(ctypes.Structure):
 
 # dfs_frag_ref as a numpy record (24 bytes: off, len, file, index).
 FRAG_REF_DTYPE = [("off", "<u8"), ("len", "<u8"), ("file", "<u4"), ("index", "<u4")]
+# dfs_xfer (48 bytes).
+XFER_DTYPE = [("phase", "<u4"), ("kind", "<u4"), ("peer", "<i4"), ("frag", "<u4"), ("from_dst", "<u4"),
+              ("reserved", "<u4"), ("src_off", "<u8"), ("dst_off", "<u8"), ("len", "<u8")]
 
 
 _vp = ctypes.c_void_p
@@ -89,6 +97,17 @@ SIGNATURES = {
     "dfs_store_bodies_receive": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_store_write_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _u32, _vp, _vp, _u32, _vp, _u32]),
     "dfs_store_read_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _u32]),
+    "dfs_comm_unique_id": (_int, [_vp]),
+    "dfs_comm_init_rank": (_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_vp)]),
+    "dfs_comm_init_all": (_int, [_vp, _u32, _vp]),
+    "dfs_comm_destroy": (_int, [_vp]),
+    "dfs_comm_info": (_int, [_vp, _vp, _vp]),
+    "dfs_comm_last_error": (ctypes.c_char_p, []),
+    "dfs_place_sizes": (_int, [_vp, _u32, _vp, _u32, _vp]),
+    "dfs_place_plan": (_int, [_u32, _u32, _u32, _vp, _u32, _u64, _vp, _vp, _vp, _vp]),
+    "dfs_place_ring": (_int, [_vp, _u32, _u32, _vp, _vp, _vp]),
+    "dfs_place_star": (_int, [_vp, _u32, _u32, _vp, _vp, _vp]),
+    "dfs_fetch_degraded": (_int, [_vp, _u32, _u32, _vp, _u64, _vp, _vp, _vp]),
 }
 
 _LIB = None

@@ -395,6 +395,19 @@ class FragmentEngine:
         return res
 
 
+def sha256_device(engine: "FragmentEngine", d_base: int, spans: np.ndarray) -> np.ndarray:
+    """dfs_sha256_batch over device memory (spans into d_base); returns the
+    (n, 32) digests on the host after the engine's stream finished."""
+    import torch
+    spans = np.ascontiguousarray(spans, dtype=np.uint64).reshape(-1, 2)
+    n = len(spans)
+    dig = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=f"cuda:{engine.device}")
+    check(lib().dfs_sha256_batch(engine.ctx, ctypes.c_void_p(d_base), _ptr(spans), n, ctypes.c_void_p(dig.data_ptr()),
+                                 L.DFS_DEVICE_PTRS), "dfs_sha256_batch")
+    torch.cuda.synchronize(engine.device)  # device-wide: the ctx stream too
+    return dig.view(-1, 32).cpu().numpy()[:n]
+
+
 def download_device(engine: "FragmentEngine", d_b64: int, spans: np.ndarray, nfiles: int, nfrag: int,
                     file_len: np.ndarray, d_exp_frag: int, d_exp_file: int, d_out: int,
                     file_off: np.ndarray) -> np.ndarray:

@@ -1,4 +1,6 @@
-"""Fragment placement across GPUs — StorageNode's replication and fetch plan.
+"""Fragment placement across GPUs — StorageNode's replication and fetch plan,
+over the C-ABI (libdfsgpu.so: dfs_comm_* / dfs_place_* / dfs_fetch_degraded,
+RCCL send/recv over xGMI).
 
 Reference (StorageNode.java, SN:line):
   * node k (0-based) stores fragments {k, (k+1) mod N}            SN:143-145, 199-200
@@ -8,32 +10,26 @@ Reference (StorageNode.java, SN:line):
 
 MI355X mapping: one process per GPU; node k is hosted by GPU k mod W (W = world
 size; with W == N, GPU g *is* node g).  Files are sharded by index over the
-ranks; each rank hashes and Base64-encodes its shard on its own GPU
-(libdfsgpu.so), with the Base64 laid out fragment-major
-(DFS_LAYOUT_FRAG_MAJOR) so the bytes bound for one node are one span.
+ranks; each rank hashes and Base64-encodes its shard on its own GPU with the
+Base64 laid out fragment-major (DFS_LAYOUT_FRAG_MAJOR), so group f (fragment f
+of every file of the rank) is one span.  After a placement every rank holds,
+for each fragment f it hosts, group f of every rank in rank order.
 
-The exchange realises the reference's pair set in two steps:
-  1. primary scatter: fragment f of every file goes to GPU(f) (point-to-point
-     sends of whole fragment groups, RCCL over xGMI on GPUs, gloo on CPU);
-  2. replica step: the primary GPU of fragment f forwards its group to the
-     GPU hosting node f-1.  With W == N this is the ring g -> g-1 of
-     BASELINE.json's north_star ("GPU g sends to g+1" under the relabelling
-     node k <-> GPU k+1), one xGMI link per GPU.
-After both steps every GPU holds exactly the fragments of the nodes it hosts.
-
-`exchange_upload_star` realises the reference's star fan-out itself as one
-all-to-all (every link busy at once); it yields the same holdings.
-
-`download_sources` mirrors SN:427-440's candidate order for a degraded fetch
-(one GPU offline) and `exchange_download` moves each requester's fragments back
-from the holders for decode + verify + reassembly (dfs_download_batch).
+Everything that moves bytes is in the library: the schedule is
+`dfs_place_plan` (pure host, also used by the CPU tests, which simulate every
+rank), the transfers are ncclSend / ncclRecv inside RCCL groups
+(`dfs_place_ring`, `dfs_place_star`, `dfs_fetch_degraded`).  This module only
+holds the pure maps, the comm setup and thin wrappers.
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+import ctypes
+from typing import Iterable, List, Optional, Sequence, Tuple
 
-import torch
-import torch.distributed as dist
+import numpy as np
+
+from . import _lib as L
+from ._lib import check, lib
 
 
 # ---------------------------------------------------------------------------
@@ -83,20 +79,17 @@ def download_sources(n: int, world: int, me: int, offline: Iterable[int] = ()) -
     return src
 
 
-# ---------------------------------------------------------------------------
-# Exchanges (torch.distributed point-to-point; RCCL on GPU, gloo on CPU)
-# ---------------------------------------------------------------------------
-def file_owner(file_digest: torch.Tensor, world: int) -> torch.Tensor:
+def file_owner(file_digest, world: int):
     """Lookup rank of files after the upload: files are
     sharded by index for hashing, but a later GET /download?fileId=<hex>
     (SN:399-403) only knows the fileId, so the owner is the digest's first 8
     bytes (big-endian, the first 16 hex chars) mod world.  file_digest:
-    (n, 32) uint8 raw digests on any device; returns (n,) int64 ranks, computed
-    where the digests live (no host round trip)."""
+    (n, 32) uint8 raw digests (torch tensor on any device); returns (n,) int64
+    ranks, computed where the digests live (no host round trip)."""
+    import torch
     d = file_digest.reshape(-1, 32)[:, :8].to(torch.int64)
-    # prefix mod world, one byte at a time: (acc * 256 + byte) mod world
     acc = torch.zeros(d.shape[0], dtype=torch.int64, device=d.device)
-    for j in range(8):
+    for j in range(8):  # prefix mod world, one byte at a time
         acc = (acc * 256 + d[:, j]) % world
     return acc
 
@@ -106,162 +99,124 @@ def file_owner_hex(file_id: str, world: int) -> int:
     return int(file_id[:16], 16) % world
 
 
-def _all_sizes(local: Sequence[int], device) -> torch.Tensor:
-    """[world, len(local)] int64 table of every rank's sizes."""
-    world = dist.get_world_size()
-    t = torch.tensor(list(local), dtype=torch.int64, device=device)
-    out = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(out, t)
-    return torch.stack(out)
+def offline_mask(offline: Iterable[int]) -> int:
+    m = 0
+    for g in offline:
+        m |= 1 << int(g)
+    return m
 
 
-def _p2p(ops: List[dist.P2POp]) -> None:
-    if ops:
-        for r in dist.batch_isend_irecv(ops):
-            r.wait()
+# ---------------------------------------------------------------------------
+# Schedules (pure host, dfs_place_plan)
+# ---------------------------------------------------------------------------
+MODES = {"ring": L.DFS_PLACE_RING, "star": L.DFS_PLACE_STAR, "fetch": L.DFS_PLACE_FETCH}
 
 
-def exchange_upload(b64: torch.Tensor, group_off: Sequence[int], nfrag: int
-                    ) -> Tuple[Dict[int, Tuple[torch.Tensor, List[int]]], List[List[int]]]:
-    """Place this rank's fragment-major Base64 on the GPUs that host its nodes.
-
-    b64        uint8 tensor, fragment-major ([fragment][file]) Base64 of the
-               rank's files (an upload plan built with frag_major=True)
-    group_off  nfrag+1 byte offsets of each fragment group inside `b64`
-    Returns (held, table): held = {f: (bytes of group f of every rank,
-    concatenated in rank order, [per-source-rank byte counts])} for every
-    fragment this GPU must hold (gpu_fragments); table[r][f] = bytes of rank
-    r's group f.
-    """
-    world, me, dev = dist.get_world_size(), dist.get_rank(), b64.device
-    sizes = [int(group_off[f + 1] - group_off[f]) for f in range(nfrag)]
-    table = _all_sizes(sizes, dev).cpu().tolist()  # table[rank][f]
-
-    def group(f):
-        return b64[int(group_off[f]):int(group_off[f + 1])]
-
-    # 1. primary scatter: fragment f -> GPU(f)
-    prim: Dict[int, torch.Tensor] = {}
-    ops = []
-    for f in range(nfrag):
-        dst = node_gpu(f, world)
-        if dst == me:
-            buf = torch.empty(sum(table[r][f] for r in range(world)), dtype=torch.uint8, device=dev)
-            o = 0
-            for r in range(world):
-                n = table[r][f]
-                if r == me:
-                    buf[o:o + n].copy_(group(f))
-                elif n:
-                    ops.append(dist.P2POp(dist.irecv, buf[o:o + n], r))
-                o += n
-            prim[f] = buf
-        elif sizes[f]:
-            ops.append(dist.P2POp(dist.isend, group(f).contiguous(), dst))
-    _p2p(ops)
-
-    # 2. replica step: GPU(f) -> GPU(node f-1)
-    held: Dict[int, Tuple[torch.Tensor, List[int]]] = {}
-    per_src = {f: [table[r][f] for r in range(world)] for f in range(nfrag)}
-    ops = []
-    for f in range(nfrag):
-        src = node_gpu(f, world)
-        dst = node_gpu(fragment_holders(f, nfrag)[1], world)
-        total = sum(per_src[f])
-        if src == me:
-            held[f] = (prim[f], per_src[f])
-            if dst != me and total:
-                ops.append(dist.P2POp(dist.isend, prim[f], dst))
-        elif dst == me:
-            buf = torch.empty(total, dtype=torch.uint8, device=dev)
-            if total:
-                ops.append(dist.P2POp(dist.irecv, buf, src))
-            held[f] = (buf, per_src[f])
-    _p2p(ops)
-    return held, table
+def plan(world: int, rank: int, nfrag: int, table: np.ndarray, mode: str, offline: Iterable[int] = ()
+         ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(ops as an XFER_DTYPE array, dst_off (nfrag+1), frag_status (nfrag)) of
+    rank `rank`'s transfer schedule; table = (world, nfrag) group bytes."""
+    t = np.ascontiguousarray(table, dtype=np.uint64).reshape(world, nfrag)
+    n = ctypes.c_uint32(0)
+    dst_off = np.zeros(nfrag + 1, dtype=np.uint64)
+    status = np.zeros(nfrag, dtype=np.int32)
+    m = offline_mask(offline)
+    check(lib().dfs_place_plan(world, rank, nfrag, t.ctypes.data, MODES[mode], m, None, ctypes.byref(n),
+                               dst_off.ctypes.data, status.ctypes.data), "dfs_place_plan")
+    ops = np.zeros(max(n.value, 1), dtype=L.XFER_DTYPE)
+    check(lib().dfs_place_plan(world, rank, nfrag, t.ctypes.data, MODES[mode], m, ops.ctypes.data, ctypes.byref(n),
+                               None, None), "dfs_place_plan")
+    return ops[:n.value], dst_off, status
 
 
-def exchange_upload_star(b64: torch.Tensor, group_off: Sequence[int], nfrag: int
-                         ) -> Tuple[Dict[int, Tuple[torch.Tensor, List[int]]], List[List[int]]]:
-    """The reference's own fan-out (SN:195-205: the uploader sends every peer
-    its pair directly) as ONE all-to-all: rank r sends GPU g the groups of
-    every fragment g must hold (gpu_fragments), so each fragment group leaves
-    its source once per holder and every xGMI link carries traffic at once
-    (SURVEY §8f rank 3), instead of the ring's scatter + forward over one
-    link.  Same result format as exchange_upload."""
-    world, me, dev = dist.get_world_size(), dist.get_rank(), b64.device
-    sizes = [int(group_off[f + 1] - group_off[f]) for f in range(nfrag)]
-    table = _all_sizes(sizes, dev).cpu().tolist()  # table[rank][f]
-    need = [gpu_fragments(g, nfrag, world) for g in range(world)]
-    parts, in_split = [], []
-    for g in range(world):
-        in_split.append(sum(sizes[f] for f in need[g]))
-        parts += [b64[int(group_off[f]):int(group_off[f + 1])] for f in need[g]]
-    send = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=dev)
-    out_split = [sum(table[r][f] for f in need[me]) for r in range(world)]
-    flat = torch.empty(sum(out_split), dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(flat, send, out_split, in_split)
-    starts = [sum(out_split[:r]) for r in range(world)]
-    recv = [flat[starts[r]:starts[r] + out_split[r]] for r in range(world)]
-    held: Dict[int, Tuple[torch.Tensor, List[int]]] = {}
-    pos = [0] * world
-    for f in need[me]:
-        per = [table[r][f] for r in range(world)]
-        pieces = []
-        for r in range(world):
-            pieces.append(recv[r][pos[r]:pos[r] + per[r]])
-            pos[r] += per[r]
-        held[f] = (torch.cat(pieces), per)
-    return held, table
+def held_layout(world: int, rank: int, nfrag: int, table: np.ndarray) -> np.ndarray:
+    """Offsets of the held groups on `rank` after a placement (UINT64_MAX =
+    not hosted); last entry = bytes of the held buffer."""
+    return plan(world, rank, nfrag, table, "star")[1]
 
 
-def exchange_download(held: Dict[int, Tuple[torch.Tensor, List[int]]], table: List[List[int]], nfrag: int,
-                      offline: Iterable[int] = (), device=None) -> Dict[int, Optional[torch.Tensor]]:
-    """Fetch this rank's fragments back from the holders (degraded read).
+def bytes_sent(ops: np.ndarray) -> int:
+    return int(ops["len"][ops["kind"] == L.DFS_XFER_SEND].sum())
 
-    Each fragment f is served by the first online holder in SN:427-428 order
-    (download_sources); the server cuts the requester's slice out of its
-    group f.  Returns {f: this rank's group-f bytes or None if no holder is
-    online}.  Offline ranks neither serve nor request.
-    """
-    world, me = dist.get_world_size(), dist.get_rank()
-    off = set(offline)
-    dev = device if device is not None else (next(iter(held.values()))[0].device if held else torch.device("cpu"))
-    out: Dict[int, Optional[torch.Tensor]] = {}
-    ops = []
-    for q in range(world):  # requester q
-        if q in off:
-            continue
-        srcs = download_sources(nfrag, world, q, off)
-        for f in range(nfrag):
-            s = srcs[f]
-            if s is None:
-                if q == me:
-                    out[f] = None
-                continue
-            if s == me:
-                buf, per = held[f]
-                lo = sum(per[:q])
-                piece = buf[lo:lo + per[q]]
-                if q == me:
-                    out[f] = piece
-                elif per[q]:
-                    ops.append(dist.P2POp(dist.isend, piece.contiguous(), q))
-            elif q == me:
-                n = table[me][f]
-                buf = torch.empty(n, dtype=torch.uint8, device=dev)
-                if n:
-                    ops.append(dist.P2POp(dist.irecv, buf, s))
-                out[f] = buf
-    _p2p(ops)
-    return out
+
+# ---------------------------------------------------------------------------
+# RCCL comms and transfers (device buffers; asynchronous on the ctx stream)
+# ---------------------------------------------------------------------------
+def _comm_error(rc: int, where: str):
+    if rc == L.DFS_E_COMM:
+        raise L.DfsError(rc, f"{where}: {lib().dfs_comm_last_error().decode(errors='replace')}")
+    check(rc, where)
+
+
+def unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * L.DFS_COMM_ID_BYTES)()
+    _comm_error(lib().dfs_comm_unique_id(buf), "dfs_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """One RCCL communicator bound to a FragmentEngine (its device and
+    stream).  Rank-per-process: Comm(engine, uid, world, rank), uid from
+    unique_id() on one rank shared out of band (e.g. torch.distributed)."""
+
+    def __init__(self, engine, uid: bytes, world: int, rank: int):
+        assert len(uid) == L.DFS_COMM_ID_BYTES
+        self.engine = engine
+        self.world, self.rank = world, rank
+        self._c = ctypes.c_void_p()
+        idb = (ctypes.c_uint8 * L.DFS_COMM_ID_BYTES).from_buffer_copy(uid)
+        _comm_error(lib().dfs_comm_init_rank(engine.ctx, idb, world, rank, ctypes.byref(self._c)),
+                    "dfs_comm_init_rank")
+
+    def _arr(self):
+        return (ctypes.c_void_p * 1)(self._c.value)
+
+    def sizes(self, grp_len: Sequence[int]) -> np.ndarray:
+        """(world, nfrag) table of every rank's group bytes (synchronous)."""
+        g = np.ascontiguousarray(grp_len, dtype=np.uint64)
+        nfrag = len(g)
+        table = np.zeros((self.world, nfrag), dtype=np.uint64)
+        _comm_error(lib().dfs_place_sizes(self._arr(), 1, g.ctypes.data, nfrag, table.ctypes.data), "dfs_place_sizes")
+        return table
+
+    def place(self, mode: str, table: np.ndarray, d_src: int, d_dst: int) -> None:
+        """Upload placement ("ring" or "star") of the fragment-major groups
+        at d_src into the held buffer d_dst (held_layout)."""
+        nfrag = table.shape[1]
+        t = np.ascontiguousarray(table, dtype=np.uint64)
+        src = (ctypes.c_void_p * 1)(d_src)
+        dst = (ctypes.c_void_p * 1)(d_dst)
+        fn = lib().dfs_place_ring if mode == "ring" else lib().dfs_place_star
+        _comm_error(fn(self._arr(), 1, nfrag, t.ctypes.data, src, dst), f"dfs_place_{mode}")
+
+    def fetch(self, table: np.ndarray, d_held: int, d_out: int, offline: Iterable[int] = ()) -> np.ndarray:
+        """Degraded read: this rank's groups back into d_out (source layout)
+        from the live holders; returns per-fragment status."""
+        nfrag = table.shape[1]
+        t = np.ascontiguousarray(table, dtype=np.uint64)
+        st = np.zeros(nfrag, dtype=np.int32)
+        src = (ctypes.c_void_p * 1)(d_held)
+        dst = (ctypes.c_void_p * 1)(d_out)
+        _comm_error(lib().dfs_fetch_degraded(self._arr(), 1, nfrag, t.ctypes.data, offline_mask(offline), src, dst,
+                                             st.ctypes.data), "dfs_fetch_degraded")
+        return st
+
+    def close(self) -> None:
+        if self._c:
+            lib().dfs_comm_destroy(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def frag_major_spans(file_lens: Sequence[int], nfrag: int):
     """(nfiles*nfrag, 2) uint64 spans of each (file, fragment) Base64 inside a
     fragment-major buffer ([fragment][file], the layout of a frag_major upload
-    plan and of the groups exchange_download returns concatenated in order)."""
-    import numpy as np
+    plan and of the groups dfs_fetch_degraded hands back)."""
     nf = len(file_lens)
     enc = np.zeros((nf, nfrag), dtype=np.uint64)
     for f, S in enumerate(file_lens):
@@ -280,6 +235,66 @@ def frag_major_spans(file_lens: Sequence[int], nfrag: int):
     return spans
 
 
-def group_sizes_table(group_off: Sequence[int], nfrag: int, device) -> List[List[int]]:
-    sizes = [int(group_off[f + 1] - group_off[f]) for f in range(nfrag)]
-    return _all_sizes(sizes, device).cpu().tolist()
+def simulate(world: int, nfrag: int, table: np.ndarray, mode: str, src: Sequence[bytes],
+             dst_in: Optional[Sequence[bytes]] = None, offline: Iterable[int] = ()) -> List[bytes]:
+    """Run every rank's dfs_place_plan schedule in one process over host
+    bytes (the matching RCCL does: per phase, rank a's sends to b pair with
+    b's receives from a in issue order).  Returns every rank's destination
+    buffer.  Used by the CPU tests and the bench's --dry-run harness check to
+    prove the schedules before they run over RCCL."""
+    plans = [plan(world, r, nfrag, table, mode, offline) for r in range(world)]
+    dst = [bytearray(int(p[1][nfrag])) for p in plans]
+    srcb = [bytes(s) for s in (dst_in if mode == "fetch" else src)]
+    phases = max([int(p[0]["phase"].max()) + 1 if len(p[0]) else 0 for p in plans] + [0])
+    for ph in range(phases):
+        snapshot = [bytes(d) for d in dst]  # a phase reads what earlier phases wrote
+        for r, (ops, _, _) in enumerate(plans):
+            for x in ops[(ops["phase"] == ph) & (ops["kind"] == L.DFS_XFER_COPY)]:
+                s = snapshot[r] if x["from_dst"] else srcb[r]
+                a, n, o = int(x["src_off"]), int(x["len"]), int(x["dst_off"])
+                dst[r][o:o + n] = s[a:a + n]
+        for a_r in range(world):
+            for b_r in range(world):
+                if a_r == b_r:
+                    continue
+                sa = plans[a_r][0]
+                sends = sa[(sa["phase"] == ph) & (sa["kind"] == L.DFS_XFER_SEND) & (sa["peer"] == b_r)]
+                rb = plans[b_r][0]
+                recvs = rb[(rb["phase"] == ph) & (rb["kind"] == L.DFS_XFER_RECV) & (rb["peer"] == a_r)]
+                if len(sends) != len(recvs):
+                    raise AssertionError(f"phase {ph}: {a_r}->{b_r} {len(sends)} sends vs {len(recvs)} recvs")
+                for x, y in zip(sends, recvs):
+                    if int(x["len"]) != int(y["len"]):
+                        raise AssertionError(f"phase {ph}: {a_r}->{b_r} send {x['len']} vs recv {y['len']}")
+                    s = snapshot[a_r] if x["from_dst"] else srcb[a_r]
+                    a, n, o = int(x["src_off"]), int(x["len"]), int(y["dst_off"])
+                    dst[b_r][o:o + n] = s[a:a + n]
+    return [bytes(d) for d in dst]
+
+
+def run_plan_torch(ops: np.ndarray, src, dst) -> None:
+    """Execute one rank's dfs_place_plan schedule with torch.distributed
+    point-to-point ops on CPU tensors (gloo): the multi-process CPU check of
+    the schedules (tests/test_dist.py, bench.py --dry-run).  GPU buffers go
+    through the library's RCCL runner (Comm.place / Comm.fetch), never here."""
+    import torch.distributed as dist
+    phases = int(ops["phase"].max()) + 1 if len(ops) else 0
+    for ph in range(phases):
+        cur = ops[ops["phase"] == ph]
+        for x in cur[cur["kind"] == L.DFS_XFER_COPY]:
+            s = dst if x["from_dst"] else src
+            a, n, o = int(x["src_off"]), int(x["len"]), int(x["dst_off"])
+            dst[o:o + n].copy_(s[a:a + n])
+        p2p = []
+        for x in cur[cur["kind"] != L.DFS_XFER_COPY]:
+            n = int(x["len"])
+            if x["kind"] == L.DFS_XFER_SEND:
+                s = dst if x["from_dst"] else src
+                a = int(x["src_off"])
+                p2p.append(dist.P2POp(dist.isend, s[a:a + n].contiguous(), int(x["peer"])))
+            else:
+                o = int(x["dst_off"])
+                p2p.append(dist.P2POp(dist.irecv, dst[o:o + n], int(x["peer"])))
+        if p2p:
+            for req in dist.batch_isend_irecv(p2p):
+                req.wait()

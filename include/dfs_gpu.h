@@ -57,6 +57,7 @@ extern "C" {
                                 /* form: the host parses it with parseJson        */
 #define DFS_E_IO (-10)          /* fragment store: Files.write / readAllBytes      */
                                 /* IOException (SN:166, 285, 466)                 */
+#define DFS_E_COMM (-11)        /* RCCL error (the peer POST failed, SN:218-221)   */
 
 /* Flags. */
 #define DFS_DEVICE_PTRS 0x1u    /* data pointers are device pointers; async       */
@@ -332,6 +333,85 @@ int dfs_upload_plan_b64_offsets(const dfs_upload_plan* plan, uint64_t* b64_off);
 int dfs_upload_plan_run(dfs_ctx* ctx, dfs_upload_plan* plan, const uint8_t* d_files,
                         uint8_t* d_file_digest, uint8_t* d_frag_digest, char* d_b64, uint32_t flags);
 int dfs_upload_plan_destroy(dfs_upload_plan* plan);
+
+/* ---- multi-GPU placement over RCCL / xGMI (SN:143-145, 195-259, 422-446) -- */
+/* One rank per GPU; node k (0-based) is hosted by rank k mod W (W = ranks).
+ * Node k stores fragments {k, (k+1) mod N} (SN:143-145), so fragment f lives
+ * on the ranks of node f and node f-1 (the download candidates nodeA / nodeB,
+ * SN:427-428).
+ *
+ * Buffers (device memory of each rank's ctx):
+ *   source "groups": a rank's Base64 in fragment-major order (an upload plan
+ *     built with DFS_LAYOUT_FRAG_MAJOR): group f = fragment f of every file
+ *     the rank uploaded, groups back to back, table[r*nfrag + f] bytes each.
+ *   "held": for every fragment f the rank hosts (ascending f) the held group
+ *     f = group f of rank 0, 1, ..., W-1 concatenated.  dfs_place_plan
+ *     returns its layout (dst_off).
+ * Comms: rank-per-process (dfs_comm_unique_id on one rank, shared out of
+ * band, then dfs_comm_init_rank on every rank) or one process driving
+ * several GPUs (dfs_comm_init_all, ncclCommInitAll).  The place / fetch
+ * calls take an array of `ncomms` comms (1 in rank-per-process mode; all of
+ * a process's comms otherwise, one source / destination pointer each) and
+ * are asynchronous on each comm's ctx stream (dfs_set_stream). */
+#define DFS_COMM_ID_BYTES 128
+typedef struct dfs_comm dfs_comm;
+int dfs_comm_unique_id(uint8_t* id /* DFS_COMM_ID_BYTES */);
+int dfs_comm_init_rank(dfs_ctx* ctx, const uint8_t* id, uint32_t nranks, uint32_t rank, dfs_comm** comm);
+int dfs_comm_init_all(dfs_ctx* const* ctxs, uint32_t n, dfs_comm** comms);
+int dfs_comm_destroy(dfs_comm* comm);
+int dfs_comm_info(const dfs_comm* comm, uint32_t* nranks, uint32_t* rank);
+/* Text of the last RCCL failure on this thread (DFS_E_COMM). */
+const char* dfs_comm_last_error(void);
+
+/* table[r*nfrag + f] = bytes of rank r's group f, gathered from every rank's
+ * grp_len (ncomms*nfrag entries, host); synchronous. */
+int dfs_place_sizes(dfs_comm* const* comms, uint32_t ncomms, const uint64_t* grp_len, uint32_t nfrag,
+                    uint64_t* table);
+
+#define DFS_PLACE_RING 0   /* primary scatter + replica step g -> g-1 (north_star's ring) */
+#define DFS_PLACE_STAR 1   /* the reference's fan-out: one all-to-all (SN:195-205)        */
+#define DFS_PLACE_FETCH 2  /* degraded read: own groups back from live holders           */
+#define DFS_XFER_SEND 0
+#define DFS_XFER_RECV 1
+#define DFS_XFER_COPY 2    /* local device-to-device copy */
+/* One transfer of a rank's schedule.  Sends read src + src_off (or, with
+ * from_dst, the rank's destination buffer: the ring's forward step);
+ * receives and copies write dst + dst_off.  Transfers of one phase run as
+ * one RCCL group; phases run in order. */
+typedef struct dfs_xfer {
+    uint32_t phase;
+    uint32_t kind;
+    int32_t peer;     /* rank, -1 for a copy */
+    uint32_t frag;
+    uint32_t from_dst;
+    uint32_t reserved;
+    uint64_t src_off;
+    uint64_t dst_off;
+    uint64_t len;
+} dfs_xfer;
+/* Pure host: the schedule rank `rank` of `nranks` runs for `mode`.
+ *   ops / *nops   in: capacity (ops may be NULL: count only), out: count
+ *   dst_off       nfrag+1: where group f lands in the destination
+ *                 (UINT64_MAX: not on this rank); dst_off[nfrag] = bytes
+ *   frag_status   FETCH: DFS_E_MISSING for a fragment no live holder has
+ *                 ("Could not retrieve fragment i", SN:443-446), else 0
+ * offline_mask: bit g = rank g is down (FETCH only; W <= 64). */
+int dfs_place_plan(uint32_t nranks, uint32_t rank, uint32_t nfrag, const uint64_t* table, uint32_t mode,
+                   uint64_t offline_mask, dfs_xfer* ops, uint32_t* nops, uint64_t* dst_off, int32_t* frag_status);
+/* Upload placement (sendFragmentsToPeers, SN:195-224) of every rank's groups
+ * into the hosts' held buffers: as a ring (primary scatter then the replica
+ * step) or as the reference's star (one all-to-all over every xGMI link).
+ * Both leave identical held buffers. */
+int dfs_place_ring(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table,
+                   const char* const* d_b64, char* const* d_held);
+int dfs_place_star(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table,
+                   const char* const* d_b64, char* const* d_held);
+/* Degraded download fetch (SN:422-446): every rank not in offline_mask gets
+ * its own groups back, in source layout, at d_out, each from the first live
+ * holder in SN:427-428 order; frag_status (ncomms*nfrag, host) as
+ * dfs_place_plan's.  Offline ranks neither serve nor request. */
+int dfs_fetch_degraded(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table,
+                       uint64_t offline_mask, const char* const* d_held, char* const* d_out, int32_t* frag_status);
 
 /* ---- synthetic data (bench / tests) -------------------------------------- */
 /* Byte o of file (first_file_index + f) is byte o mod 8 (little endian) of

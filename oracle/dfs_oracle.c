@@ -360,3 +360,116 @@ double oracle_cpu_upload_bench(uint64_t seed, uint32_t nfiles, uint64_t flen, ui
     free(t);
     return j.err ? -2.0 : j.busy;
 }
+
+/* Download-side CPU baseline (bench.py cpu_baseline leg, download object):
+ * per file, what the GPU download path computes — Base64-decode every
+ * fragment (SN:281), SHA-256 it against the upload-time digest (SN:282,
+ * 248-257), ordered append into the file (SN:448-451), SHA-256 of the
+ * rebuilt file against the fileId (SN:454-458).  The Base64 and the expected
+ * digests are prepared per file outside the timed part (they stand for the
+ * fetched fragments and the digest table).  Returns the slowest worker's
+ * busy seconds, or < 0 on error / mismatch. */
+/* Table-driven decode of the body units, 4 chars -> 3 bytes per step (the
+ * shape of the JDK's non-intrinsic decodeBlock), falling back to the exact
+ * state machine above for the final unit and for any invalid input. */
+static int8_t g_dec[256];
+static pthread_once_t g_dec_once = PTHREAD_ONCE_INIT;
+static void dec_init(void) {
+    for (int c = 0; c < 256; c++) g_dec[c] = (int8_t)(b64_val((unsigned char)c) >= 0 ? b64_val((unsigned char)c) : -1);
+}
+static int fast_b64_decode(const char* in, uint64_t len, uint8_t* out, uint64_t* out_len) {
+    pthread_once(&g_dec_once, dec_init);
+    const unsigned char* s = (const unsigned char*)in;
+    if (len < 8 || (len & 3)) return oracle_b64_decode(in, len, out, out_len);
+    uint64_t units = len / 4 - 1, dp = 0;
+    for (uint64_t u = 0; u < units; u++) {
+        const int a = g_dec[s[4 * u]], b = g_dec[s[4 * u + 1]], c = g_dec[s[4 * u + 2]], d = g_dec[s[4 * u + 3]];
+        if ((a | b | c | d) < 0) return oracle_b64_decode(in, len, out, out_len);
+        const uint32_t v = (uint32_t)a << 18 | (uint32_t)b << 12 | (uint32_t)c << 6 | (uint32_t)d;
+        out[dp] = (uint8_t)(v >> 16); out[dp + 1] = (uint8_t)(v >> 8); out[dp + 2] = (uint8_t)v;
+        dp += 3;
+    }
+    uint64_t tail = 0;
+    if (oracle_b64_decode(in + 4 * units, 4, out + dp, &tail) != 0) return oracle_b64_decode(in, len, out, out_len);
+    *out_len = dp + tail;
+    return 0;
+}
+
+typedef struct {
+    uint64_t seed; uint32_t nfiles; uint64_t flen; uint32_t nfrag; sha_fn sha;
+    uint32_t next; pthread_mutex_t mu; double busy; int err;
+} cpu_dl_job;
+
+static void* cpu_dl_worker(void* p) {
+    cpu_dl_job* j = (cpu_dl_job*)p;
+    const uint32_t N = j->nfrag;
+    uint8_t* file = (uint8_t*)malloc(j->flen ? j->flen : 1);
+    uint8_t* out = (uint8_t*)malloc(j->flen ? j->flen : 1);
+    uint64_t fcap = j->flen / N + 1;
+    uint8_t* frag = (uint8_t*)malloc(fcap + 3);
+    char* b64 = (char*)malloc(N * (4 * ((fcap + 2) / 3)) + 16);
+    uint64_t* off = (uint64_t*)malloc(8 * N);
+    uint64_t* len = (uint64_t*)malloc(8 * N);
+    uint64_t* boff = (uint64_t*)malloc(8 * (N + 1));
+    uint8_t* exp = (uint8_t*)malloc(32 * (N + 1));
+    double busy = 0;
+    int err = 0;
+    if (!file || !out || !frag || !b64 || !off || !len || !boff || !exp) { err = 1; goto done; }
+    oracle_split(j->flen, N, off, len);
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        uint32_t f = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (f >= j->nfiles) break;
+        oracle_synth(j->seed, f, 0, j->flen, file);
+        boff[0] = 0;
+        for (uint32_t i = 0; i < N; i++) {
+            boff[i + 1] = boff[i] + oracle_b64_encode(file + off[i], len[i], b64 + boff[i]);
+            j->sha(file + off[i], len[i], exp + 32 * i);
+        }
+        j->sha(file, j->flen, exp + 32 * N);
+        double t0 = now_s();
+        uint64_t o = 0;
+        for (uint32_t i = 0; i < N; i++) {
+            uint64_t got = 0;
+            uint8_t d[32];
+            if (fast_b64_decode(b64 + boff[i], boff[i + 1] - boff[i], frag, &got) != 0) err = 1; /* SN:281 */
+            j->sha(frag, got, d);                                                                  /* SN:282 */
+            if (memcmp(d, exp + 32 * i, 32) != 0) err = 1;                                        /* SN:250-257 */
+            memcpy(out + o, frag, got);                                                            /* SN:448 */
+            o += got;
+        }
+        uint8_t d[32];
+        j->sha(out, o, d);                                   /* SN:454 */
+        if (memcmp(d, exp + 32 * N, 32) != 0) err = 1;       /* SN:455-458 */
+        busy += now_s() - t0;
+    }
+done:
+    pthread_mutex_lock(&j->mu);
+    if (busy > j->busy) j->busy = busy;
+    if (err) j->err = 1;
+    pthread_mutex_unlock(&j->mu);
+    free(file); free(out); free(frag); free(b64); free(off); free(len); free(boff); free(exp);
+    return 0;
+}
+
+double oracle_cpu_download_bench(uint64_t seed, uint32_t nfiles, uint64_t flen, uint32_t nfrag, int threads,
+                                 int use_openssl) {
+    sha_fn sha = oracle_sha256;
+    if (use_openssl) {
+        if (!g_ossl_sha256) {
+            void* h = dlopen("libcrypto.so.3", RTLD_NOW);
+            if (!h) h = dlopen("libcrypto.so", RTLD_NOW);
+            if (h) g_ossl_sha256 = (openssl_sha256_t)dlsym(h, "SHA256");
+        }
+        if (!g_ossl_sha256) return -1.0;
+        sha = sha_openssl;
+    }
+    cpu_dl_job j = {seed, nfiles, flen, nfrag, sha, 0, PTHREAD_MUTEX_INITIALIZER, 0.0, 0};
+    if (threads < 1) threads = 1;
+    pthread_t* t = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    for (int i = 0; i < threads; i++) pthread_create(&t[i], 0, cpu_dl_worker, &j);
+    for (int i = 0; i < threads; i++) pthread_join(t[i], 0);
+    free(t);
+    return j.err ? -2.0 : j.busy;
+}

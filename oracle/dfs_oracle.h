@@ -80,6 +80,13 @@ void oracle_synth(uint64_t seed, uint64_t file_index, uint64_t start, uint64_t l
 double oracle_cpu_upload_bench(uint64_t seed, uint32_t nfiles, uint64_t file_len,
                                uint32_t nfrag, int threads, int use_openssl,
                                uint8_t* file_digest_out, uint8_t* frag_digest_out);
+/* Download-side CPU baseline: per file, Base64-decode each fragment (SN:281),
+ * SHA-256 it against the upload digest (SN:282), ordered append (SN:448),
+ * SHA-256 of the file against its fileId (SN:454).  Seconds of the slowest
+ * worker (fragment Base64 and expected digests prepared untimed), < 0 on
+ * error or mismatch. */
+double oracle_cpu_download_bench(uint64_t seed, uint32_t nfiles, uint64_t file_len, uint32_t nfrag,
+                                 int threads, int use_openssl);
 
 #ifdef __cplusplus
 }

@@ -59,6 +59,9 @@ def lib() -> ctypes.CDLL:
     L.oracle_cpu_upload_bench.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                           ctypes.c_int, ctypes.c_int, u8p, u8p]
     L.oracle_cpu_upload_bench.restype = ctypes.c_double
+    L.oracle_cpu_download_bench.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_int, ctypes.c_int]
+    L.oracle_cpu_download_bench.restype = ctypes.c_double
     _LIB = L
     return L
 
@@ -131,6 +134,14 @@ def cpu_upload_bench(nfiles: int, file_len: int, nfrag: int, threads: int, use_o
     secs = lib().oracle_cpu_upload_bench(seed, nfiles, file_len, nfrag, threads, int(use_openssl),
                                          fd.ctypes.data, frd.ctypes.data)
     return secs, fd, frd
+
+
+def cpu_download_bench(nfiles: int, file_len: int, nfrag: int, threads: int, use_openssl: bool,
+                       seed: int = SYNTH_SEED) -> float:
+    """Seconds spent on the download path (decode + fragment SHA-256 verify +
+    ordered append + fileId SHA-256 verify) for `nfiles` synthetic files;
+    < 0 on error."""
+    return lib().oracle_cpu_download_bench(seed, nfiles, file_len, nfrag, threads, int(use_openssl))
 
 
 # --------------------------------------------------------------------------

@@ -1,12 +1,13 @@
-"""Multi-rank placement (gloo on CPU, world 2, 4 and 8; 8 ranks x 5 nodes is
-the bench's 8-GPU replication leg, GPUs 5-7 hosting no node).
+"""Multi-rank placement (gloo on CPU, world 2, 4 and 8).
 
-Checks that the replication exchange leaves every rank holding exactly the
-fragments of the nodes it hosts (node k stores {k, k+1}, SN:143-145,
-196-205), bit-exact, and that a degraded read with one rank offline fetches
-every fragment from the surviving holder (SN:422-446).  The Base64 payloads
-come from the CPU oracle; the exchange code is the same module bench.py runs
-over RCCL on GPUs.
+Checks that the library's transfer schedules (dfs_place_plan: ring, star,
+degraded fetch), executed by separate processes over gloo point-to-point,
+leave every rank holding exactly the fragments of the nodes it hosts (node k
+stores {k, k+1}, SN:143-145, 196-205), bit-exact, and that a degraded read
+with one rank offline fetches every fragment from the surviving holder
+(SN:422-446).  The Base64 payloads come from the CPU oracle; on GPUs the same
+schedules run over RCCL inside libdfsgpu.so (dfs_place_ring / _star /
+dfs_fetch_degraded).
 """
 import os
 import socket
@@ -57,38 +58,48 @@ def _worker(rank, world, port, nfrag, nfiles, offline, q):
         from dfs_amd import placement as P
         files = _rank_files(rank, nfiles)
         blob, off, _ = _frag_major(files, nfrag)
-        t = torch.frombuffer(bytearray(blob or b"\0"), dtype=torch.uint8)[:len(blob)]
-        held, table = P.exchange_upload(t, off, nfrag)
-        # expected: group f of every rank in rank order, for my fragments
+        src = torch.frombuffer(bytearray(blob or b"\0"), dtype=torch.uint8)[:len(blob)]
+        # the size table every rank agrees on (dfs_place_sizes over RCCL on GPUs)
+        sizes = torch.tensor([off[f + 1] - off[f] for f in range(nfrag)], dtype=torch.int64)
+        rows = [torch.empty_like(sizes) for _ in range(world)]
+        dist.all_gather(rows, sizes)
+        table = np.stack([r.numpy() for r in rows]).astype(np.uint64)
         want = P.gpu_fragments(rank, nfrag, world)
-        assert sorted(held) == want, (sorted(held), want)
-        for f in want:
-            exp = b"".join(_frag_major(_rank_files(r, nfiles), nfrag)[2][f] for r in range(world))
-            got = held[f][0].numpy().tobytes()
-            assert got == exp, (rank, f)
-            assert held[f][1] == [table[r][f] for r in range(world)]
-        # the star fan-out as one all-to-all yields the same holdings
-        star, table2 = P.exchange_upload_star(t, off, nfrag)
-        assert table2 == table and sorted(star) == want
-        for f in want:
-            assert torch.equal(star[f][0], held[f][0]) and star[f][1] == held[f][1], (rank, f)
-        # degraded read: my own fragments back from the holders
-        got = P.exchange_download(held, table, nfrag, offline=offline)
+        held = {}
+        for mode in ("ring", "star"):
+            ops, lay, _ = P.plan(world, rank, nfrag, table, mode)
+            dst = torch.zeros(int(lay[nfrag]), dtype=torch.uint8)
+            P.run_plan_torch(ops, src, dst)
+            for f in want:
+                exp = b"".join(_frag_major(_rank_files(r, nfiles), nfrag)[2][f] for r in range(world))
+                o = int(lay[f])
+                assert dst[o:o + len(exp)].numpy().tobytes() == exp, (mode, rank, f)
+            held[mode] = dst
+        assert torch.equal(held["ring"], held["star"])
+        # degraded read: my own groups back from the live holders
+        ops, lay, st = P.plan(world, rank, nfrag, table, "fetch", offline)
+        out = torch.zeros(int(lay[nfrag]), dtype=torch.uint8)
+        P.run_plan_torch(ops, held["star"], out)
         if rank not in offline:
             mine = _frag_major(files, nfrag)[2]
             for f in range(nfrag):
-                assert got[f] is not None and got[f].numpy().tobytes() == mine[f], (rank, f)
+                if st[f] == 0:
+                    assert out[int(lay[f]):int(lay[f]) + len(mine[f])].numpy().tobytes() == mine[f], (rank, f)
+                else:
+                    assert P.download_sources(nfrag, world, rank, offline)[f] is None
         dist.barrier()
         dist.destroy_process_group()
         q.put((rank, "ok"))
-    except Exception as e:  # report to the parent
+    except Exception:  # report to the parent
         import traceback
         q.put((rank, traceback.format_exc()))
 
 
 @pytest.mark.parametrize("world,nfrag,offline", [(2, 5, ()), (2, 5, (1,)), (4, 4, ()), (4, 4, (2,)), (4, 8, (0,)),
-                                                       (4, 3, (3,)), (8, 5, (7,))])
+                                                       (4, 3, (3,)), (8, 5, (7,)), (8, 8, (3,))])
 def test_placement_exchange(world, nfrag, offline):
+    """dfs_place_plan's ring / star / fetch schedules executed by real
+    processes over gloo point-to-point (the RCCL runner issues the same ops)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

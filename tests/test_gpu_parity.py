@@ -386,7 +386,7 @@ def test_align128_plan(monkeypatch, mode):
 def test_frag_major_plan_and_device_download(engine):
     """The single-GPU half of bench.py's placement leg: a fragment-major
     upload plan, then dfs_download_batch on device pointers over the
-    concatenated groups (what exchange_download hands back)."""
+    concatenated groups (what dfs_fetch_degraded hands back)."""
     import torch
     from dfs_amd import placement as P
     from dfs_amd.engine import download_device
@@ -417,6 +417,58 @@ def test_frag_major_plan_and_device_download(engine):
     assert (st == 0).all()
     assert torch.equal(out, files[:nfiles * S])
     plan.close()
+
+
+def test_rccl_placement_single_rank(engine):
+    """The RCCL path of the C-ABI placement on one GPU (world 1: every node on
+    rank 0): comm init from a unique id, the size all-gather, ring and star
+    placement, then the degraded fetch hands back the rank's own groups in
+    source layout and dfs_download_batch rebuilds and verifies every file.
+    Multi-rank schedules are checked on the CPU (tests/test_placement_plan.py,
+    tests/test_dist.py); the driver's 8-GPU bench runs them over xGMI."""
+    import torch
+    from dfs_amd import placement as P
+    from dfs_amd.engine import download_device
+    nfiles, S, nfrag = 33, 40007, 5
+    spans = np.array([(f * S, S) for f in range(nfiles)], dtype=np.uint64)
+    files = torch.empty(nfiles * S + 8, dtype=torch.uint8, device="cuda")
+    dfs_amd.synth_fill(engine, files.data_ptr(), spans, 900, O.SYNTH_SEED)
+    plan = dfs_amd.UploadPlan(engine, spans, nfrag, frag_major=True)
+    fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
+    frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
+    b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+    plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
+    torch.cuda.synchronize()
+    offs = plan.b64_offsets()
+    grp = [int(offs[f]) for f in range(nfrag)] + [int(offs[-1])]  # group f starts with file 0's fragment f
+    comm = P.Comm(engine, P.unique_id(), 1, 0)
+    try:
+        table = comm.sizes([grp[f + 1] - grp[f] for f in range(nfrag)])
+        assert table.tolist() == [[grp[f + 1] - grp[f] for f in range(nfrag)]]
+        lay = P.held_layout(1, 0, nfrag, table)
+        held = {}
+        for mode in ("ring", "star"):
+            h = torch.zeros(int(lay[nfrag]), dtype=torch.uint8, device="cuda")
+            comm.place(mode, table, b64.data_ptr(), h.data_ptr())
+            torch.cuda.synchronize()
+            held[mode] = h
+        assert torch.equal(held["ring"], held["star"])
+        assert torch.equal(held["star"], b64[:int(lay[nfrag])])  # one rank holds every group as uploaded
+        back = torch.zeros_like(b64)
+        st = comm.fetch(table, held["star"].data_ptr(), back.data_ptr())
+        torch.cuda.synchronize()
+        assert (st == 0).all() and torch.equal(back, b64)
+        out = torch.zeros(nfiles * S, dtype=torch.uint8, device="cuda")
+        status = download_device(engine, back.data_ptr(), plan.b64_spans([S] * nfiles), nfiles, nfrag,
+                                 np.full(nfiles, S, np.uint64), frd.data_ptr(), fd.data_ptr(), out.data_ptr(),
+                                 np.arange(nfiles, dtype=np.uint64) * np.uint64(S))
+        assert (status == 0).all() and torch.equal(out, files[:nfiles * S])
+        # the only rank offline: every fragment is missing (SN:443-446)
+        assert (comm.fetch(table, held["star"].data_ptr(), back.data_ptr(), offline=[0]) ==
+                dfs_amd.DFS_E_MISSING).all()
+    finally:
+        comm.close()
+        plan.close()
 
 
 def test_sha256_update_streaming(engine, golden):

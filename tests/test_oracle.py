@@ -162,3 +162,12 @@ def test_cpu_bench_matches_oracle(threads):
     s2, fd2, frd2 = O.cpu_upload_bench(6, 4096 + 3, 5, threads, use_openssl=True)
     if s2 >= 0:  # libcrypto present
         assert (fd2 == fd).all() and (frd2 == frd).all()
+
+
+def test_cpu_download_baseline_verifies():
+    """The download-side CPU baseline decodes, hashes and reassembles every
+    file and checks every digest itself (< 0 on any mismatch)."""
+    for n in (0, 1, 2, 7, 100, 4097, 1000003):
+        for ossl in (False, True):
+            secs = O.cpu_download_bench(3, n, 5, 2, ossl)
+            assert secs >= 0 or (ossl and secs == -1.0), (n, ossl, secs)
