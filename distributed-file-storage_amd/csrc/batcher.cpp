@@ -1,0 +1,441 @@
+// batcher.cpp — request batcher in front of the fragment pipeline
+// (include/dfs_gpu.h, dfs_batcher_* / dfs_submit_*).
+//
+// Reference: StorageNode runs one thread per connection (StorageNode.java
+// :28-31) and every handler processes one file: handleUpload (:118-189) and
+// handleDownload (:399-461).  A GPU launch per file would be floored by that
+// file's fileId chain and leave the chip almost empty, so concurrent handler
+// calls are coalesced: a handler thread submits its one file and blocks; a
+// worker takes every request queued within a short window (or until a batch
+// is full) and runs them as one launch.
+//
+// Workers: `depth` threads, each with its own dfs_ctx (stream + scratch),
+// pinned host staging and device buffers, so batch k+1's copies and launch
+// overlap batch k's kernels.  The handler threads copy their own bytes into
+// and out of the pinned staging, so those copies run in parallel instead of
+// on the worker.  Host-resident data crosses PCIe twice (file in, Base64
+// out for uploads; Base64 in, file out for downloads): that, not the
+// kernels, bounds a host-buffer caller at high concurrency.
+//
+// Hand-off per request (all under the batcher mutex):
+//   0 queued -> 1 worker assigned its staging slot (in_dst) -> 2 handler
+//   copied its input in -> 3 results ready (out_src, status) -> 4 handler
+//   copied its output out; the worker reuses the staging only after every
+//   request of its batch reached 4.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/dfs_gpu.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
+
+struct Req;
+
+struct BatchSync {
+    std::condition_variable cv;  // a handler advanced its request
+};
+
+enum Kind { kUpload = 0, kDownload = 1 };  // download kinds: 1 + (exp_frag ? 2 : 0) + (exp_file ? 1 : 0)
+
+struct Req {
+    int kind = kUpload;
+    uint64_t len = 0;        // file bytes
+    uint64_t need = 0;       // input bytes staged (upload: len; download: Base64 chars)
+    uint64_t out_bytes = 0;  // output bytes copied back (upload: Base64; download: len)
+    // upload
+    const uint8_t* file = nullptr;
+    uint8_t* fd = nullptr;
+    uint8_t* frd = nullptr;
+    char* b64 = nullptr;
+    uint64_t* b64_off = nullptr;
+    // download
+    const char* text = nullptr;
+    const dfs_span* frags = nullptr;
+    const uint8_t* exp_frag = nullptr;
+    const uint8_t* exp_file = nullptr;
+    uint8_t* out = nullptr;
+    // hand-off
+    Clock::time_point arrive;
+    int phase = 0;
+    BatchSync* sync = nullptr;
+    uint8_t* in_dst = nullptr;         // staging slot of the input
+    const uint8_t* out_src = nullptr;  // staging of the output
+    int status = DFS_OK;
+    std::condition_variable cv;
+};
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    int grow(size_t n) {
+        if (n <= cap) return DFS_OK;
+        const size_t want = std::max<size_t>({n, cap + cap / 2, size_t(1) << 20});
+        void* q = nullptr;
+        if ((pinned ? hipHostMalloc(&q, want, hipHostMallocDefault) : hipMalloc(&q, want)) != hipSuccess)
+            return DFS_E_NOMEM;
+        release();
+        p = q;
+        cap = want;
+        return DFS_OK;
+    }
+    void release() {
+        if (p) (void)(pinned ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct Worker {
+    dfs_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    Buf pin_in, pin_out, d_in, d_out, d_dig;
+    std::thread th;
+    Worker() {
+        pin_in.pinned = pin_out.pinned = true;
+    }
+};
+
+}  // namespace
+
+struct dfs_batcher {
+    int device = 0;
+    uint32_t nfrag = 5;
+    dfs_batcher_opts o{};
+    std::mutex mu;
+    std::condition_variable cv_work;
+    std::deque<Req*> q;
+    uint64_t q_bytes = 0;
+    bool stop = false;
+    std::vector<Worker*> workers;
+    uint64_t n_batches = 0, n_requests = 0, max_batch = 0;
+};
+
+namespace {
+
+// Give every request its staging slot and wait until all copied their input.
+void stage_in(dfs_batcher* B, std::vector<Req*>& batch, BatchSync& bs, uint8_t* base,
+              const std::vector<uint64_t>& off) {
+    std::unique_lock<std::mutex> lk(B->mu);
+    for (size_t i = 0; i < batch.size(); ++i) {
+        batch[i]->in_dst = base + off[i];
+        batch[i]->phase = 1;
+        batch[i]->cv.notify_one();
+    }
+    bs.cv.wait(lk, [&] {
+        for (Req* r : batch)
+            if (r->phase < 2) return false;
+        return true;
+    });
+}
+
+int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs) {
+    const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
+    std::vector<dfs_span> spans(n);
+    std::vector<uint64_t> in_off(n);
+    uint64_t total = 0, b64_total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        in_off[i] = total;
+        spans[i] = dfs_span{total, batch[i]->len};
+        total += (batch[i]->len + 15) & ~15ull;  // 16-byte aligned file starts
+        b64_total += batch[i]->b64_off[N];       // filled at submit: the request's Base64 bytes
+    }
+    const uint64_t dig_bytes = 32ull * n * (N + 1);
+    int rc = w.pin_in.grow(total + 16);
+    if (!rc) rc = w.pin_out.grow(dig_bytes + b64_total + 16);
+    if (!rc) rc = w.d_in.grow(total + 16);
+    if (!rc) rc = w.d_out.grow(b64_total + 16);
+    if (!rc) rc = w.d_dig.grow(dig_bytes);
+    if (rc) return rc;
+    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off);
+    std::vector<uint64_t> b64_off(static_cast<uint64_t>(n) * N + 1);
+    uint8_t* d_fd = w.d_dig.as<uint8_t>();
+    uint8_t* d_frd = d_fd + 32ull * n;
+    if (total && hipMemcpyAsync(w.d_in.p, w.pin_in.p, total, hipMemcpyHostToDevice, w.stream) != hipSuccess)
+        return DFS_E_HIP;
+    rc = dfs_upload_batch(w.ctx, w.d_in.as<uint8_t>(), spans.data(), n, N, d_fd, d_frd, w.d_out.as<char>(),
+                          b64_total, b64_off.data(), DFS_DEVICE_PTRS);
+    if (rc) return rc;
+    uint8_t* h = w.pin_out.as<uint8_t>();
+    if (hipMemcpyAsync(h, d_fd, dig_bytes, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
+        (b64_total && hipMemcpyAsync(h + dig_bytes, w.d_out.p, b64_total, hipMemcpyDeviceToHost, w.stream) != hipSuccess) ||
+        hipStreamSynchronize(w.stream) != hipSuccess)
+        return DFS_E_HIP;
+    for (uint32_t i = 0; i < n; ++i) {
+        Req* r = batch[i];
+        std::memcpy(r->fd, h + 32ull * i, 32);
+        std::memcpy(r->frd, h + 32ull * n + 32ull * N * i, 32ull * N);
+        r->out_src = h + dig_bytes + b64_off[static_cast<uint64_t>(i) * N];  // its Base64, [fragment] order
+    }
+    return DFS_OK;
+}
+
+int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs) {
+    const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
+    const bool have_f = batch.front()->exp_frag != nullptr, have_i = batch.front()->exp_file != nullptr;
+    std::vector<uint64_t> in_off(n), file_len(n), file_off(n);
+    std::vector<dfs_span> spans(static_cast<uint64_t>(n) * N);
+    std::vector<uint8_t> ef(have_f ? 32ull * n * N : 0), ei(have_i ? 32ull * n : 0);
+    uint64_t total = 0, out_total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const Req* r = batch[i];
+        in_off[i] = total;
+        uint64_t o = total;  // the handler packs its fragments back to back
+        for (uint32_t k = 0; k < N; ++k) {
+            const dfs_span& s = r->frags[k];
+            dfs_span& d = spans[static_cast<uint64_t>(i) * N + k];
+            if (s.len == DFS_SPAN_MISSING) {
+                d = s;
+            } else {
+                d = dfs_span{o, s.len};
+                o += s.len;
+            }
+        }
+        total += (r->need + 15) & ~15ull;
+        file_len[i] = r->len;
+        file_off[i] = out_total;
+        out_total += (r->len + 15) & ~15ull;
+        if (have_f) std::memcpy(ef.data() + 32ull * N * i, r->exp_frag, 32ull * N);
+        if (have_i) std::memcpy(ei.data() + 32ull * i, r->exp_file, 32);
+    }
+    int rc = w.pin_in.grow(total + 16);
+    if (!rc) rc = w.pin_out.grow(out_total + 16);
+    if (!rc) rc = w.d_in.grow(total + 16);
+    if (!rc) rc = w.d_out.grow(out_total + 16);
+    if (rc) return rc;
+    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off);
+    if (total && hipMemcpyAsync(w.d_in.p, w.pin_in.p, total, hipMemcpyHostToDevice, w.stream) != hipSuccess)
+        return DFS_E_HIP;
+    std::vector<int32_t> st(n);
+    rc = dfs_download_batch(w.ctx, w.d_in.as<char>(), spans.data(), n, N, file_len.data(), have_f ? ef.data() : nullptr,
+                            have_i ? ei.data() : nullptr, w.d_out.as<uint8_t>(), file_off.data(), st.data(),
+                            DFS_DEVICE_PTRS);
+    if (rc != DFS_OK && rc != DFS_E_MISSING && rc != DFS_E_DECODE && rc != DFS_E_FRAG_MISMATCH && rc != DFS_E_CORRUPT)
+        return rc;
+    if (out_total && (hipMemcpyAsync(w.pin_out.p, w.d_out.p, out_total, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
+                      hipStreamSynchronize(w.stream) != hipSuccess))
+        return DFS_E_HIP;
+    for (uint32_t i = 0; i < n; ++i) {
+        batch[i]->status = st[i];
+        batch[i]->out_src = w.pin_out.as<uint8_t>() + file_off[i];
+    }
+    return DFS_OK;
+}
+
+void worker_main(dfs_batcher* B, Worker* w) {
+    (void)hipSetDevice(B->device);
+    const auto window = std::chrono::microseconds(B->o.max_wait_us);
+    for (;;) {
+        std::vector<Req*> batch;
+        BatchSync bs;
+        {
+            std::unique_lock<std::mutex> lk(B->mu);
+            B->cv_work.wait(lk, [&] { return B->stop || !B->q.empty(); });
+            if (B->q.empty()) return;  // stopping and drained
+            // the window opens with the oldest request; a full queue goes at once
+            while (!B->stop && !B->q.empty() && B->q.size() < B->o.max_files && B->q_bytes < B->o.max_bytes &&
+                   Clock::now() < B->q.front()->arrive + window)
+                B->cv_work.wait_until(lk, B->q.front()->arrive + window);
+            if (B->q.empty()) continue;  // another worker took them
+            const int kind = B->q.front()->kind;
+            uint64_t bytes = 0;
+            for (auto it = B->q.begin(); it != B->q.end() && batch.size() < B->o.max_files;) {
+                Req* r = *it;
+                if (r->kind != kind || (!batch.empty() && bytes + r->need > B->o.max_bytes)) {
+                    ++it;
+                    continue;
+                }
+                r->sync = &bs;
+                batch.push_back(r);
+                bytes += r->need;
+                B->q_bytes -= r->need;
+                it = B->q.erase(it);
+            }
+            ++B->n_batches;
+            B->n_requests += batch.size();
+            B->max_batch = std::max<uint64_t>(B->max_batch, batch.size());
+            if (!B->q.empty()) B->cv_work.notify_one();
+        }
+        const int rc = batch.front()->kind == kUpload ? run_uploads(B, *w, batch, bs) : run_downloads(B, *w, batch, bs);
+        // Results ready (or the batch failed); reuse the staging only after
+        // every handler copied its output out.
+        std::unique_lock<std::mutex> lk(B->mu);
+        for (Req* r : batch) {
+            if (rc != DFS_OK) {
+                r->status = rc;
+                r->out_src = nullptr;
+            }
+            r->phase = 3;
+            r->cv.notify_one();
+        }
+        bs.cv.wait(lk, [&] {
+            for (Req* r : batch)
+                if (r->phase < 4) return false;
+            return true;
+        });
+    }
+}
+
+// The handler side of one request: enqueue, copy the input into the
+// staging slot when the worker hands it out, wait for the results, copy the
+// output out of the staging.
+int submit(dfs_batcher* B, Req& r) {
+    r.arrive = Clock::now();
+    std::unique_lock<std::mutex> lk(B->mu);
+    if (B->stop) return DFS_E_ARG;
+    B->q.push_back(&r);
+    B->q_bytes += r.need;
+    B->cv_work.notify_one();
+    r.cv.wait(lk, [&] { return r.phase >= 1; });
+    if (r.phase == 1) {
+        lk.unlock();
+        if (r.kind == kUpload) {
+            if (r.len) std::memcpy(r.in_dst, r.file, r.len);
+        } else {  // the fragments' Base64 back to back (run_downloads rebases the spans)
+            uint8_t* d = r.in_dst;
+            for (uint32_t k = 0; k < B->nfrag; ++k) {
+                const dfs_span& s = r.frags[k];
+                if (s.len == DFS_SPAN_MISSING || !s.len) continue;
+                std::memcpy(d, r.text + s.off, s.len);
+                d += s.len;
+            }
+        }
+        lk.lock();
+        r.phase = 2;
+        r.sync->cv.notify_one();
+    }
+    r.cv.wait(lk, [&] { return r.phase >= 3; });
+    if (r.out_src && r.out_bytes && (r.kind == kUpload || r.status == DFS_OK)) {
+        lk.unlock();
+        std::memcpy(r.kind == kUpload ? static_cast<void*>(r.b64) : static_cast<void*>(r.out), r.out_src, r.out_bytes);
+        lk.lock();
+    }
+    r.phase = 4;
+    r.sync->cv.notify_one();
+    return r.status;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfs_batcher_create(int device, uint32_t nfrag, const dfs_batcher_opts* opts, dfs_batcher** out) {
+    if (!out || !nfrag || nfrag > 64) return DFS_E_ARG;
+    *out = nullptr;
+    auto* B = new (std::nothrow) dfs_batcher;
+    if (!B) return DFS_E_NOMEM;
+    B->device = device;
+    B->nfrag = nfrag;
+    B->o = dfs_batcher_opts{200, 1024, 1ull << 30, 2};
+    if (opts) {
+        if (opts->max_wait_us) B->o.max_wait_us = opts->max_wait_us;
+        if (opts->max_files) B->o.max_files = opts->max_files;
+        if (opts->max_bytes) B->o.max_bytes = opts->max_bytes;
+        if (opts->depth) B->o.depth = std::min<uint32_t>(opts->depth, 8);
+    }
+    int rc = DFS_OK;
+    for (uint32_t i = 0; i < B->o.depth && rc == DFS_OK; ++i) {
+        auto* w = new (std::nothrow) Worker;
+        if (!w) {
+            rc = DFS_E_NOMEM;
+            break;
+        }
+        B->workers.push_back(w);
+        rc = dfs_open(&w->ctx, device);
+        if (rc == DFS_OK && hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) rc = DFS_E_HIP;
+        if (rc == DFS_OK) rc = dfs_set_stream(w->ctx, w->stream);
+    }
+    if (rc == DFS_OK)
+        for (Worker* w : B->workers) w->th = std::thread(worker_main, B, w);
+    if (rc != DFS_OK) {
+        dfs_batcher_destroy(B);
+        return rc;
+    }
+    *out = B;
+    return DFS_OK;
+}
+
+int dfs_batcher_destroy(dfs_batcher* B) {
+    if (!B) return DFS_E_ARG;
+    {
+        std::lock_guard<std::mutex> lk(B->mu);
+        B->stop = true;
+    }
+    B->cv_work.notify_all();
+    for (Worker* w : B->workers) {
+        if (w->th.joinable()) w->th.join();
+        (void)hipSetDevice(B->device);
+        for (Buf* b : {&w->pin_in, &w->pin_out, &w->d_in, &w->d_out, &w->d_dig}) b->release();
+        if (w->ctx) dfs_close(w->ctx);
+        if (w->stream) (void)hipStreamDestroy(w->stream);
+        delete w;
+    }
+    delete B;
+    return DFS_OK;
+}
+
+int dfs_batcher_stats(dfs_batcher* B, uint64_t* batches, uint64_t* requests, uint64_t* max_batch) {
+    if (!B) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(B->mu);
+    if (batches) *batches = B->n_batches;
+    if (requests) *requests = B->n_requests;
+    if (max_batch) *max_batch = B->max_batch;
+    return DFS_OK;
+}
+
+int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t* file_digest, uint8_t* frag_digest,
+                      char* b64, uint64_t b64_cap, uint64_t* b64_off) {
+    if (!B || (len && !file) || !file_digest || !frag_digest || !b64_off) return DFS_E_ARG;
+    const uint32_t N = B->nfrag;
+    dfs_span fr[64];
+    if (dfs_split_plan(len, N, fr) != DFS_OK) return DFS_E_ARG;
+    b64_off[0] = 0;
+    for (uint32_t i = 0; i < N; ++i) b64_off[i + 1] = b64_off[i] + enc_len(fr[i].len);  // SN:636
+    if (b64_off[N] > b64_cap || (b64_off[N] && !b64)) return DFS_E_ARG;
+    Req r;
+    r.kind = kUpload;
+    r.file = file;
+    r.len = r.need = len;
+    r.out_bytes = b64_off[N];
+    r.fd = file_digest;
+    r.frd = frag_digest;
+    r.b64 = b64;
+    r.b64_off = b64_off;
+    return submit(B, r);
+}
+
+int dfs_submit_download(dfs_batcher* B, const char* b64, const dfs_span* frags, uint64_t file_len,
+                        const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest, uint8_t* out) {
+    if (!B || !frags || (file_len && !out)) return DFS_E_ARG;
+    Req r;
+    r.kind = kDownload + (expected_frag_digest ? 2 : 0) + (expected_file_digest ? 1 : 0);
+    uint64_t need = 0;
+    for (uint32_t k = 0; k < B->nfrag; ++k)
+        if (frags[k].len != DFS_SPAN_MISSING) need += frags[k].len;
+    if (need && !b64) return DFS_E_ARG;
+    r.text = b64;
+    r.frags = frags;
+    r.len = file_len;
+    r.need = need;
+    r.out_bytes = file_len;
+    r.exp_frag = expected_frag_digest;
+    r.exp_file = expected_file_digest;
+    r.out = out;
+    return submit(B, r);
+}
+
+}  // extern "C"

@@ -234,6 +234,15 @@ int put(dfs_ctx* c, int id, const void* src, size_t n, hipStream_t s) {
     return DFS_OK;
 }
 
+bool is_device_ptr(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // plain host memory: clear the sticky error
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
 int enter(dfs_ctx* c) {
     if (!c) return DFS_E_ARG;
     HIPC(hipSetDevice(c->device));
@@ -647,62 +656,60 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
 
 // ---------------------------------------------------------------------------
 // Upload plan: descriptors built once on the host, uploaded once.
-int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint32_t flags,
-                           dfs_upload_plan** out, uint64_t* b64_total) {
-    if (!c || !out || !nfrag || (nfiles && !files)) return DFS_E_ARG;
-    if (flags & ~(DFS_LAYOUT_FRAG_MAJOR | DFS_LAYOUT_ALIGN128)) return DFS_E_ARG;
+}  // extern "C"
+
+namespace {
+
+// The host half of an upload plan: SHA lanes (fileIds + fragments, and the
+// fragments alone), encode jobs, Base64 layout.
+struct HostPlan {
+    std::vector<ShaDesc> all, frag;
+    std::vector<StreamJob> enc;
+    std::vector<uint64_t> b64_off;
+    uint32_t prio_all = 0, prio_frag = 0;
+    uint64_t enc_tiles = 0, total = 0;
+};
+
+int build_host_plan(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint32_t flags, HostPlan& h) {
     const bool frag_major = flags & DFS_LAYOUT_FRAG_MAJOR;
     const uint64_t align = (flags & DFS_LAYOUT_ALIGN128) ? 128 : 1;
-    *out = nullptr;
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (int rc = enter(c)) return rc;
-    auto* p = new (std::nothrow) dfs_upload_plan;
-    if (!p) return DFS_E_NOMEM;
-    p->device = c->device;
-    p->nfiles = nfiles;
-    p->nfrag = nfrag;
     const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
-    if (nfiles + nf > 0xffffffffull) {
-        delete p;
-        return DFS_E_ARG;
-    }
-    std::vector<ShaDesc> all, frag;
-    all.reserve(nfiles + nf);
-    frag.reserve(nf);
-    std::vector<StreamJob> enc;
+    if (nfiles + nf > 0xffffffffull) return DFS_E_ARG;
+    h.all.clear();
+    h.frag.clear();
+    h.enc.clear();
+    h.all.reserve(nfiles + nf);
+    h.frag.reserve(nf);
     std::vector<uint64_t> items;
-    enc.reserve(nf + 1);
+    h.enc.reserve(nf + 1);
     items.reserve(nf);
-    p->b64_off.resize(nf + 1);
+    h.b64_off.assign(nf + 1, 0);
     std::vector<uint64_t> off(nfrag), len(nfrag);
     for (uint32_t f = 0; f < nfiles; ++f) {
-        if (files[f].len >= kMaxMsg) {
-            delete p;
-            return DFS_E_ARG;
-        }
-        all.push_back(msg(files[f].off, files[f].len, f));  // fileId, SN:127
-        split(files[f].len, nfrag, off.data(), len.data());          // SN:138-157
+        if (files[f].len >= kMaxMsg) return DFS_E_ARG;
+        h.all.push_back(msg(files[f].off, files[f].len, f));  // fileId, SN:127
+        split(files[f].len, nfrag, off.data(), len.data());   // SN:138-157
         for (uint32_t i = 0; i < nfrag; ++i) {
             const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
             const ShaDesc d = msg(files[f].off + off[i], len[i], nfiles + k);  // SN:159
-            all.push_back(d);
-            frag.push_back(d);
+            h.all.push_back(d);
+            h.frag.push_back(d);
         }
     }
     // Base64 layout: [file][fragment] (default) or [fragment][file].
     uint64_t total = 0;
     auto place = [&](uint32_t f, uint32_t i) {
         const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
-        const ShaDesc& d = frag[k];
+        const ShaDesc& d = h.frag[k];
         total = (total + align - 1) / align * align;
-        p->b64_off[k] = total;
+        h.b64_off[k] = total;
         if (d.len) {
             StreamJob j{};
             j.src_off = d.off;
             j.len = d.len;
             j.dst_off = total;
             j.id = static_cast<uint32_t>(k);
-            enc.push_back(j);
+            h.enc.push_back(j);
             items.push_back((d.len + 11) / 12);
         }
         total += enc_len(d.len);  // SN:636
@@ -714,37 +721,83 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
         for (uint32_t f = 0; f < nfiles; ++f)
             for (uint32_t i = 0; i < nfrag; ++i) place(f, i);
     }
-    p->b64_off[nf] = total;
-    p->b64_total = total;
+    h.b64_off[nf] = total;
+    h.total = total;
     // Fragment lanes carry their Base64 offset: the fused upload encodes in
     // the SHA pass (kShaB64 is ignored when the kernel gets no output).
-    for (std::vector<ShaDesc>* v : {&all, &frag})
+    for (std::vector<ShaDesc>* v : {&h.all, &h.frag})
         for (ShaDesc& d : *v)
             if (d.out >= nfiles) {
-                d.b64 = p->b64_off[d.out - nfiles];
+                d.b64 = h.b64_off[d.out - nfiles];
                 d.flags |= dfs::kShaB64;
             }
-    p->prio_all = sort_lanes(all);
-    p->prio_frag = sort_lanes(frag);
-    p->n_all = static_cast<uint32_t>(all.size());
-    p->n_frag_only = static_cast<uint32_t>(frag.size());
-    p->n_enc = static_cast<uint32_t>(enc.size());
-    p->enc_tiles = finish_jobs(enc, items, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
+    h.prio_all = sort_lanes(h.all);
+    h.prio_frag = sort_lanes(h.frag);
+    h.enc_tiles = finish_jobs(h.enc, items, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
+    return DFS_OK;
+}
+
+void fill_plan_header(dfs_upload_plan* p, const HostPlan& h, int device, uint32_t nfiles, uint32_t nfrag) {
+    p->device = device;
+    p->nfiles = nfiles;
+    p->nfrag = nfrag;
+    p->prio_all = h.prio_all;
+    p->prio_frag = h.prio_frag;
+    p->n_all = static_cast<uint32_t>(h.all.size());
+    p->n_frag_only = static_cast<uint32_t>(h.frag.size());
+    p->n_enc = static_cast<uint32_t>(h.enc.size() - 1);  // minus the sentinel
+    p->enc_tiles = h.enc_tiles;
+    p->b64_total = h.total;
+}
+
+// A plan whose device tables live in the ctx scratch (valid until the next
+// call on the ctx): one-shot batches (dfs_upload_batch, the batcher) pay no
+// hipMalloc / hipFree per call.  Asynchronous on the ctx stream.
+int scratch_plan(dfs_ctx* c, const HostPlan& h, uint32_t nfiles, uint32_t nfrag, hipStream_t s, dfs_upload_plan& p) {
+    fill_plan_header(&p, h, c->device, nfiles, nfrag);
+    if (int rc = put(c, B_DESC, h.all.data(), h.all.size() * sizeof(ShaDesc), s)) return rc;
+    if (int rc = put(c, B_JOBS2, h.frag.data(), h.frag.size() * sizeof(ShaDesc), s)) return rc;
+    if (int rc = put(c, B_JOBS, h.enc.data(), h.enc.size() * sizeof(StreamJob), s)) return rc;
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    p.d_all = c->buf[B_DESC].as<ShaDesc>();
+    p.d_frag = c->buf[B_JOBS2].as<ShaDesc>();
+    p.d_enc = c->buf[B_JOBS].as<StreamJob>();
+    p.d_queue = c->buf[B_QUEUE].as<uint32_t>();
+    return DFS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint32_t flags,
+                           dfs_upload_plan** out, uint64_t* b64_total) {
+    if (!c || !out || !nfrag || (nfiles && !files)) return DFS_E_ARG;
+    if (flags & ~(DFS_LAYOUT_FRAG_MAJOR | DFS_LAYOUT_ALIGN128)) return DFS_E_ARG;
+    *out = nullptr;
+    HostPlan h;
+    if (int rc = build_host_plan(files, nfiles, nfrag, flags, h)) return rc;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    auto* p = new (std::nothrow) dfs_upload_plan;
+    if (!p) return DFS_E_NOMEM;
+    fill_plan_header(p, h, c->device, nfiles, nfrag);
+    p->b64_off = std::move(h.b64_off);
     hipError_t e = hipMalloc(&p->d_queue, dfs::kShaQueueBytes);
-    if (e == hipSuccess) e = hipMalloc(&p->d_all, std::max<size_t>(all.size(), 1) * sizeof(ShaDesc));
-    if (e == hipSuccess) e = hipMalloc(&p->d_frag, std::max<size_t>(frag.size(), 1) * sizeof(ShaDesc));
-    if (e == hipSuccess) e = hipMalloc(&p->d_enc, enc.size() * sizeof(StreamJob));
-    if (e == hipSuccess && !all.empty())
-        e = hipMemcpy(p->d_all, all.data(), all.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
-    if (e == hipSuccess && !frag.empty())
-        e = hipMemcpy(p->d_frag, frag.data(), frag.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&p->d_all, std::max<size_t>(h.all.size(), 1) * sizeof(ShaDesc));
+    if (e == hipSuccess) e = hipMalloc(&p->d_frag, std::max<size_t>(h.frag.size(), 1) * sizeof(ShaDesc));
+    if (e == hipSuccess) e = hipMalloc(&p->d_enc, h.enc.size() * sizeof(StreamJob));
+    if (e == hipSuccess && !h.all.empty())
+        e = hipMemcpy(p->d_all, h.all.data(), h.all.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !h.frag.empty())
+        e = hipMemcpy(p->d_frag, h.frag.data(), h.frag.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
     if (e == hipSuccess)
-        e = hipMemcpy(p->d_enc, enc.data(), enc.size() * sizeof(StreamJob), hipMemcpyHostToDevice);
+        e = hipMemcpy(p->d_enc, h.enc.data(), h.enc.size() * sizeof(StreamJob), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         dfs_upload_plan_destroy(p);
         return hip_fail(e, "dfs_upload_plan_create");
     }
-    if (b64_total) *b64_total = total;
+    if (b64_total) *b64_total = p->b64_total;
     *out = p;
     return DFS_OK;
 }
@@ -834,16 +887,11 @@ int dfs_upload_batch(dfs_ctx* c, const uint8_t* files, const dfs_span* spans, ui
                      uint8_t* fd, uint8_t* frd, char* b64, uint64_t b64_cap, uint64_t* b64_off, uint32_t flags) {
     if (!c || !nfrag || (nfiles && (!spans || !frd))) return DFS_E_ARG;
     if (!(flags & DFS_NO_FILEID) && nfiles && !fd) return DFS_E_ARG;
-    dfs_upload_plan* p = nullptr;
-    uint64_t total = 0;
-    if (int rc = dfs_upload_plan_create(c, spans, nfiles, nfrag, flags & DFS_LAYOUT_FRAG_MAJOR, &p, &total)) return rc;
-    struct Guard {
-        dfs_upload_plan* p;
-        ~Guard() { dfs_upload_plan_destroy(p); }
-    } guard{p};
+    HostPlan h;
+    if (int rc = build_host_plan(spans, nfiles, nfrag, flags & DFS_LAYOUT_FRAG_MAJOR, h)) return rc;
     const bool do_b64 = !(flags & DFS_NO_B64);
-    if (b64_off) std::memcpy(b64_off, p->b64_off.data(), p->b64_off.size() * sizeof(uint64_t));
-    if (do_b64 && (total > b64_cap || (total && !b64))) return DFS_E_ARG;
+    if (b64_off) std::memcpy(b64_off, h.b64_off.data(), h.b64_off.size() * sizeof(uint64_t));
+    if (do_b64 && (h.total > b64_cap || (h.total && !b64))) return DFS_E_ARG;
     if (!nfiles) return DFS_OK;
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = enter(c)) return rc;
@@ -866,17 +914,19 @@ int dfs_upload_batch(dfs_ctx* c, const uint8_t* files, const dfs_span* spans, ui
         d_fd = c->buf[B_DIG0].as<uint8_t>();
         d_frd = c->buf[B_DIG1].as<uint8_t>();
         if (do_b64) {
-            HIPC(c->buf[B_DATA_OUT].ensure(total));
+            HIPC(c->buf[B_DATA_OUT].ensure(h.total));
             d_b64 = c->buf[B_DATA_OUT].as<char>();
         }
     }
-    if (int rc = run_plan_locked(c, p, d_files, d_fd, d_frd, d_b64, flags)) return rc;
+    dfs_upload_plan p;
+    if (int rc = scratch_plan(c, h, nfiles, nfrag, s, p)) return rc;
+    if (int rc = run_plan_locked(c, &p, d_files, d_fd, d_frd, d_b64, flags)) return rc;
     if (!dev) {
         if (!(flags & DFS_NO_FILEID)) HIPC(hipMemcpyAsync(fd, d_fd, 32ull * nfiles, hipMemcpyDeviceToHost, s));
         HIPC(hipMemcpyAsync(frd, d_frd, 32ull * nf, hipMemcpyDeviceToHost, s));
-        if (do_b64 && total) HIPC(hipMemcpyAsync(b64, d_b64, total, hipMemcpyDeviceToHost, s));
+        if (do_b64 && h.total) HIPC(hipMemcpyAsync(b64, d_b64, h.total, hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
     }
-    HIPC(hipStreamSynchronize(s));  // the plan is freed on return
     return DFS_OK;
 }
 
@@ -1057,14 +1107,14 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     std::vector<uint8_t> expf, expd;
-    if (dev && exp_frag) {  // expected digests may be device pointers in device mode
+    if (dev && exp_frag && is_device_ptr(exp_frag)) {  // expected digests may live on the device in device mode
         expf.resize(32ull * nf);
-        HIPC(hipMemcpy(expf.data(), exp_frag, expf.size(), hipMemcpyDefault));
+        HIPC(hipMemcpy(expf.data(), exp_frag, expf.size(), hipMemcpyDeviceToHost));
         exp_frag = expf.data();
     }
-    if (dev && exp_file) {
+    if (dev && exp_file && is_device_ptr(exp_file)) {
         expd.resize(32ull * nfiles);
-        HIPC(hipMemcpy(expd.data(), exp_file, expd.size(), hipMemcpyDefault));
+        HIPC(hipMemcpy(expd.data(), exp_file, expd.size(), hipMemcpyDeviceToHost));
         exp_file = expd.data();
     }
     int rc = DFS_OK;

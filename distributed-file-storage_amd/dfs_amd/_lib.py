@@ -52,6 +52,11 @@ class dfs_span(ctypes.Structure):
     _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint64)]
 
 
+class dfs_batcher_opts(ctypes.Structure):
+    _fields_ = [("max_wait_us", ctypes.c_uint32), ("max_files", ctypes.c_uint32), ("max_bytes", ctypes.c_uint64),
+                ("depth", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
 # dfs_frag_ref as a numpy record (24 bytes: off, len, file, index).
 FRAG_REF_DTYPE = [("off", "<u8"), ("len", "<u8"), ("file", "<u4"), ("index", "<u4")]
 # dfs_xfer (48 bytes).
@@ -97,6 +102,11 @@ SIGNATURES = {
     "dfs_store_bodies_receive": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_store_write_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _u32, _vp, _vp, _u32, _vp, _u32]),
     "dfs_store_read_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _u32]),
+    "dfs_batcher_create": (_int, [_int, _u32, _vp, ctypes.POINTER(_vp)]),
+    "dfs_batcher_destroy": (_int, [_vp]),
+    "dfs_batcher_stats": (_int, [_vp, _vp, _vp, _vp]),
+    "dfs_submit_upload": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
+    "dfs_submit_download": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "dfs_comm_unique_id": (_int, [_vp]),
     "dfs_comm_init_rank": (_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_vp)]),
     "dfs_comm_init_all": (_int, [_vp, _u32, _vp]),

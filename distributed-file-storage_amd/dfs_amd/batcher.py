@@ -1,0 +1,89 @@
+"""Request batcher (dfs_batcher_* / dfs_submit_*): StorageNode's
+thread-per-connection handlers (SN:28-31) each submit ONE file; the library
+coalesces concurrent submissions into one launch.  Calls release the GIL
+(ctypes), so Python threads stand in for the Java handler threads."""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import check, dfs_batcher_opts, lib
+
+
+class Batcher:
+    def __init__(self, device: int, nfrag: int, max_wait_us: int = 0, max_files: int = 0, max_bytes: int = 0,
+                 depth: int = 0):
+        self.nfrag = nfrag
+        self._b = ctypes.c_void_p()
+        o = dfs_batcher_opts(max_wait_us, max_files, max_bytes, depth, 0)
+        check(lib().dfs_batcher_create(device, nfrag, ctypes.byref(o), ctypes.byref(self._b)), "dfs_batcher_create")
+
+    def upload_into(self, data: np.ndarray, fd: np.ndarray, frd: np.ndarray, b64: np.ndarray,
+                    b64_off: np.ndarray) -> int:
+        """handleUpload's pipeline for one file into caller buffers (no copies
+        on the Python side): fd (32,), frd (nfrag, 32), b64, b64_off
+        (nfrag + 1,) uint8/uint64 arrays.  Returns the DFS status."""
+        return lib().dfs_submit_upload(self._b, data.ctypes.data if data.size else None, data.size, fd.ctypes.data,
+                                       frd.ctypes.data, b64.ctypes.data if b64.size else None, b64.size,
+                                       b64_off.ctypes.data)
+
+    def upload(self, data: bytes) -> Tuple[bytes, list, list]:
+        """(fileId digest, fragment digests, fragment Base64 strings)."""
+        a = np.frombuffer(data, dtype=np.uint8)
+        n = len(data)
+        cap = sum(4 * ((n // self.nfrag + 1 + 2) // 3) for _ in range(self.nfrag)) + 16
+        fd = np.zeros(32, np.uint8)
+        frd = np.zeros((self.nfrag, 32), np.uint8)
+        b64 = np.zeros(cap, np.uint8)
+        off = np.zeros(self.nfrag + 1, np.uint64)
+        check(self.upload_into(a, fd, frd, b64, off), "dfs_submit_upload")
+        return (fd.tobytes(), [frd[i].tobytes() for i in range(self.nfrag)],
+                [b64[int(off[i]):int(off[i + 1])].tobytes() for i in range(self.nfrag)])
+
+    def download(self, b64_frags: Sequence[Optional[bytes]], file_len: int, frag_digests: Optional[Sequence[bytes]],
+                 file_digest: Optional[bytes]) -> Tuple[int, Optional[bytes]]:
+        """Base64 download of one file: (status, bytes or None)."""
+        texts = [t for t in b64_frags if t is not None]
+        buf = np.frombuffer(b"".join(texts) or b"\0", dtype=np.uint8)
+        spans = (L.dfs_span * self.nfrag)()
+        o = 0
+        for i, t in enumerate(b64_frags):
+            if t is None:
+                spans[i].off, spans[i].len = 0, L.DFS_SPAN_MISSING
+            else:
+                spans[i].off, spans[i].len = o, len(t)
+                o += len(t)
+        ef = np.frombuffer(b"".join(frag_digests), np.uint8) if frag_digests is not None else None
+        ei = np.frombuffer(file_digest, np.uint8) if file_digest is not None else None
+        out = np.zeros(max(file_len, 1), np.uint8)
+        st = lib().dfs_submit_download(self._b, buf.ctypes.data, spans, file_len,
+                                       ef.ctypes.data if ef is not None else None,
+                                       ei.ctypes.data if ei is not None else None, out.ctypes.data)
+        if st not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_DECODE, L.DFS_E_FRAG_MISMATCH, L.DFS_E_CORRUPT):
+            check(st, "dfs_submit_download")
+        return st, (out[:file_len].tobytes() if st == 0 else None)
+
+    def stats(self) -> dict:
+        b, r, m = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib().dfs_batcher_stats(self._b, ctypes.byref(b), ctypes.byref(r), ctypes.byref(m)), "dfs_batcher_stats")
+        return {"batches": b.value, "requests": r.value, "max_batch": m.value}
+
+    def close(self) -> None:
+        if self._b:
+            lib().dfs_batcher_destroy(self._b)
+            self._b = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

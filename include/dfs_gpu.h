@@ -334,6 +334,41 @@ int dfs_upload_plan_run(dfs_ctx* ctx, dfs_upload_plan* plan, const uint8_t* d_fi
                         uint8_t* d_file_digest, uint8_t* d_frag_digest, char* d_b64, uint32_t flags);
 int dfs_upload_plan_destroy(dfs_upload_plan* plan);
 
+/* ---- request batcher: thread-per-connection callers (SN:28-31) ---------- */
+/* StorageNode's handlers each process ONE file (handleUpload SN:118-189,
+ * handleDownload SN:399-461) on their own thread.  A batcher coalesces the
+ * concurrent calls: dfs_submit_* blocks the calling thread, a worker runs
+ * every request queued within max_wait_us of the oldest (or until max_files
+ * / max_bytes) as one launch, and `depth` workers keep batches in flight
+ * (each has its own ctx, stream, pinned staging and device buffers).  All
+ * buffers are host memory; the caller's bytes are copied by its own thread
+ * into / out of pinned staging.  Thread-safe; results are bit-identical to
+ * dfs_upload_batch / dfs_download_batch on the same file.  Zero fields of
+ * opts take the defaults (200 us, 1024 files, 1 GiB, depth 2). */
+typedef struct dfs_batcher dfs_batcher;
+typedef struct dfs_batcher_opts {
+    uint32_t max_wait_us;
+    uint32_t max_files;
+    uint64_t max_bytes;
+    uint32_t depth;
+    uint32_t reserved;
+} dfs_batcher_opts;
+int dfs_batcher_create(int device, uint32_t nfrag, const dfs_batcher_opts* opts, dfs_batcher** batcher);
+/* Stops accepting requests, finishes the queued ones, joins the workers. */
+int dfs_batcher_destroy(dfs_batcher* batcher);
+int dfs_batcher_stats(dfs_batcher* batcher, uint64_t* batches, uint64_t* requests, uint64_t* max_batch);
+/* One upload (SN:127, 138-159, 636): file_digest[32], frag_digest[nfrag*32],
+ * the fragments' Base64 back to back in b64 (b64_off[nfrag+1], relative). */
+int dfs_submit_upload(dfs_batcher* batcher, const uint8_t* file, uint64_t len, uint8_t* file_digest,
+                      uint8_t* frag_digest, char* b64, uint64_t b64_cap, uint64_t* b64_off);
+/* One download with Base64 transport (SN:281-282, 422-458): frags[nfrag]
+ * spans into b64 (len DFS_SPAN_MISSING = no holder had it); out = file_len
+ * bytes; returns 0 / DFS_E_MISSING / DFS_E_DECODE / DFS_E_FRAG_MISMATCH /
+ * DFS_E_CORRUPT as dfs_download_batch's status.  Expected digests may be
+ * NULL (not checked). */
+int dfs_submit_download(dfs_batcher* batcher, const char* b64, const dfs_span* frags, uint64_t file_len,
+                        const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest, uint8_t* out);
+
 /* ---- multi-GPU placement over RCCL / xGMI (SN:143-145, 195-259, 422-446) -- */
 /* One rank per GPU; node k (0-based) is hosted by rank k mod W (W = ranks).
  * Node k stores fragments {k, (k+1) mod N} (SN:143-145), so fragment f lives

@@ -1,0 +1,106 @@
+"""Request batcher (dfs_batcher / dfs_submit_*): many handler threads, one file
+each (StorageNode's thread-per-connection model, SN:28-31), coalesced into
+batched launches.  Every result is checked bit-exact against the CPU oracle:
+uploads (fileId, fragment digests, fragment Base64) and downloads (bytes,
+and the reference's failure statuses)."""
+import threading
+
+import numpy as np
+import pytest
+
+import dfs_amd
+import oracle as O
+from dfs_amd.batcher import Batcher
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 2, 4, 5, 7, 28, 55, 56, 64, 119, 467, 2154, 9506, 65535, 1 << 20, (1 << 20) + 3, 3 << 20]
+
+
+def _file(i):
+    return O.c_synth(7000 + i, 0, SIZES[i % len(SIZES)] if i < 2 * len(SIZES) else 1000 + 37 * i)
+
+
+def _run_threads(n, fn):
+    errs = []
+    start = threading.Barrier(n)
+
+    def body(t):
+        try:
+            start.wait()
+            fn(t)
+        except Exception as e:  # collected, reported by the main thread
+            import traceback
+            errs.append(traceback.format_exc())
+    ths = [threading.Thread(target=body, args=(t,)) for t in range(n)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=300)
+    assert not errs, errs[0]
+
+
+@pytest.mark.parametrize("nfrag", [5, 8])
+def test_concurrent_uploads_and_downloads_vs_oracle(nfrag):
+    threads, per = 64, 3
+    with Batcher(0, nfrag, max_wait_us=2000) as b:
+        results = {}
+
+        def work(t):
+            for k in range(per):
+                i = t * per + k
+                data = _file(i)
+                fd, frd, texts = b.upload(data)
+                efd, efrd, eb64, eoff = O.c_upload_batch([data], nfrag)
+                assert fd == efd[0].tobytes(), i
+                assert frd == [efrd[0, j].tobytes() for j in range(nfrag)], i
+                assert b"".join(texts) == eb64, i
+                st, back = b.download(texts, len(data), frd, fd)
+                assert st == 0 and back == data, (i, st)
+                results[i] = True
+        _run_threads(threads, work)
+        assert len(results) == threads * per
+        s = b.stats()
+        assert s["requests"] == 2 * threads * per
+        assert s["batches"] < s["requests"]  # concurrent calls were coalesced
+        assert s["max_batch"] > 1
+
+
+def test_download_failure_statuses_and_mixed_expectations():
+    nfrag = 5
+    with Batcher(0, nfrag, max_wait_us=2000) as b:
+        data = O.c_synth(42, 0, 100003)
+        fd, frd, texts = b.upload(data)
+        cases = []
+        cases.append(("ok", texts, frd, fd, 0))
+        cases.append(("no expectations", texts, None, None, 0))
+        cases.append(("file digest only", texts, None, fd, 0))
+        miss = list(texts)
+        miss[2] = None
+        cases.append(("missing", miss, frd, fd, dfs_amd.DFS_E_MISSING))       # SN:443-446
+        bad = list(texts)
+        bad[1] = bad[1][:10] + b"*" + bad[1][11:]
+        cases.append(("bad char", bad, frd, fd, dfs_amd.DFS_E_DECODE))        # SN:281 IAE
+        wrong = list(frd)
+        wrong[3] = bytes(32)
+        cases.append(("frag digest", texts, wrong, fd, dfs_amd.DFS_E_FRAG_MISMATCH))  # SN:250-257
+        cases.append(("file digest", texts, frd, bytes(32), dfs_amd.DFS_E_CORRUPT))  # SN:455-458
+        out = {}
+
+        def work(t):
+            name, tx, ef, ei, want = cases[t % len(cases)]
+            st, back = b.download(tx, len(data), ef, ei)
+            out[t] = (name, st, want, back == data if st == 0 else back is None)
+        _run_threads(4 * len(cases), work)
+        for t, (name, st, want, good) in out.items():
+            assert st == want and good, (name, st, want)
+
+
+def test_single_request_latency_path():
+    """One handler alone: the batch of one still runs (window expires)."""
+    with Batcher(0, 5, max_wait_us=100) as b:
+        data = O.c_synth(3, 0, 1 << 20)
+        fd, frd, texts = b.upload(data)
+        efd, efrd, eb64, _ = O.c_upload_batch([data], 5)
+        assert fd == efd[0].tobytes() and b"".join(texts) == eb64
+        assert b.stats()["batches"] == 1
