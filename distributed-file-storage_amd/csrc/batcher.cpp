@@ -19,9 +19,9 @@
 //
 // Hand-off per request (all under the batcher mutex):
 //   0 queued -> 1 worker assigned its staging slot (in_dst) -> 2 handler
-//   copied its input in -> 3 results ready (out_src, status) -> 4 handler
-//   copied its output out; the worker reuses the staging only after every
-//   request of its batch reached 4.
+//   copied its input in (BatchSync::copied_in) -> 3 results ready (out_src,
+//   status) -> 4 handler copied its output out (BatchSync::copied_out); the
+//   worker reuses the staging only after every request of its batch did.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,8 +44,14 @@ uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
 
 struct Req;
 
+// Lives on the worker's stack for one batch.  Handlers only touch it (under
+// the batcher mutex) before their submit returns; the worker leaves the
+// batch only after `copied_out` reached the batch size, so it outlives
+// every use.  Requests themselves live on the handlers' stacks: the worker
+// never reads a request once its handler may have returned.
 struct BatchSync {
     std::condition_variable cv;  // a handler advanced its request
+    size_t copied_in = 0, copied_out = 0;
 };
 
 enum Kind { kUpload = 0, kDownload = 1 };  // download kinds: 1 + (exp_frag ? 2 : 0) + (exp_file ? 1 : 0)
@@ -136,11 +142,7 @@ void stage_in(dfs_batcher* B, std::vector<Req*>& batch, BatchSync& bs, uint8_t* 
         batch[i]->phase = 1;
         batch[i]->cv.notify_one();
     }
-    bs.cv.wait(lk, [&] {
-        for (Req* r : batch)
-            if (r->phase < 2) return false;
-        return true;
-    });
+    bs.cv.wait(lk, [&] { return bs.copied_in == batch.size(); });
 }
 
 int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs) {
@@ -282,11 +284,8 @@ void worker_main(dfs_batcher* B, Worker* w) {
             r->phase = 3;
             r->cv.notify_one();
         }
-        bs.cv.wait(lk, [&] {
-            for (Req* r : batch)
-                if (r->phase < 4) return false;
-            return true;
-        });
+        const size_t n = batch.size();
+        bs.cv.wait(lk, [&] { return bs.copied_out == n; });
     }
 }
 
@@ -316,6 +315,7 @@ int submit(dfs_batcher* B, Req& r) {
         }
         lk.lock();
         r.phase = 2;
+        ++r.sync->copied_in;
         r.sync->cv.notify_one();
     }
     r.cv.wait(lk, [&] { return r.phase >= 3; });
@@ -325,8 +325,10 @@ int submit(dfs_batcher* B, Req& r) {
         lk.lock();
     }
     r.phase = 4;
+    const int status = r.status;
+    ++r.sync->copied_out;
     r.sync->cv.notify_one();
-    return r.status;
+    return status;
 }
 
 }  // namespace

@@ -12,7 +12,7 @@ import dfs_amd
 import oracle as O
 from dfs_amd.batcher import Batcher
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(120)]
 
 SIZES = [0, 1, 2, 4, 5, 7, 28, 55, 56, 64, 119, 467, 2154, 9506, 65535, 1 << 20, (1 << 20) + 3, 3 << 20]
 
