@@ -453,106 +453,57 @@ def store_leg(args, eng, files, fd, S, N, F, dev, log):
 def batcher_leg(args, log):
     """Thread-per-connection clients (SN:28-31), one 1 MiB file per request,
     through the library's batcher (dfs_submit_upload / dfs_submit_download,
-    host buffers: PCIe in and out), at each concurrency in --clients; closed
-    loop for --client-seconds.  Beside it the CPU proxy at the same
-    concurrency (min(C, cores) threads, one file per thread).  Results of
-    every client's first request are checked with hashlib / base64."""
-    import base64
+    host buffers: PCIe in and out) at each concurrency in --clients, closed
+    loop for --client-seconds.  The clients are native threads
+    (tools/batcher_load, a child process); the fileIds it reports are checked
+    here.  Beside it the CPU proxy at the same concurrency (min(C, cores)
+    threads, one file per thread)."""
     import hashlib
-    import threading
-    import numpy as np
-    from dfs_amd.batcher import Batcher
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O  # cpu_baseline leg only
+    import oracle as O  # checker + cpu_baseline leg only
     S, N = 1 << 20, 5
+    tool = os.path.join(ROOT, "tools", "batcher_load")
     _, cores = host_cpu_info()
-    rng = np.random.default_rng(5)
-    distinct = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(64)]
-    b = Batcher(0, N, max_wait_us=500, max_files=1024, max_bytes=1 << 30, depth=3)
-    # Base64 + digests of the distinct files for the download clients
-    ref = [b.upload(d.tobytes()) for d in distinct]
-    good = [True]
-    rows = []
-    cpu_one = None
+    want = [hashlib.sha256(O.c_synth(f, 0, S)).hexdigest() for f in (0, 1)]
+    rows, ok, cpu_one = [], True, None
     for C in [int(x) for x in args.clients.split(",") if x]:
         row = {"clients": C}
         for kind in ("upload", "download"):
-            lat = []
-            lock = threading.Lock()
-            deadline = [0.0]
-            start = threading.Barrier(C + 1)
-
-            def client(t):
-                d = distinct[t % 64]
-                fd = np.zeros(32, np.uint8)
-                frd = np.zeros((N, 32), np.uint8)
-                bb = np.zeros(4 * ((S // N + 3) // 3) * N + 64, np.uint8)
-                off = np.zeros(N + 1, np.uint64)
-                mine = []
-                first = True
-                start.wait()
-                while True:
-                    t0 = time.perf_counter()
-                    if kind == "upload":
-                        st = b.upload_into(d, fd, frd, bb, off)
-                    else:
-                        fdr, frdr, texts = ref[t % 64]
-                        st, back = b.download(texts, S, frdr, fdr)
-                    t1 = time.perf_counter()
-                    mine.append(t1 - t0)
-                    if first:
-                        first = False
-                        if kind == "upload":
-                            raw = d.tobytes()
-                            ok = st == 0 and fd.tobytes() == hashlib.sha256(raw).digest() and \
-                                bb[:int(off[N])].tobytes() == b"".join(
-                                    base64.b64encode(raw[o:o + n]) for o, n in O.py_split(S, N))
-                        else:
-                            ok = st == 0 and back == d.tobytes()
-                        if not ok:
-                            good[0] = False
-                    if t1 >= deadline[0]:
-                        break
-                with lock:
-                    lat.extend(mine)
-            ths = [threading.Thread(target=client, args=(t,), daemon=True) for t in range(C)]
-            for th in ths:
-                th.start()
-            deadline[0] = time.perf_counter() + args.client_seconds
-            t0 = time.perf_counter()
-            start.wait()
-            for th in ths:
-                th.join()
-            wall = time.perf_counter() - t0
-            lat_ms = np.array(lat) * 1e3
-            row[kind] = {"requests": len(lat), "gbps": round(len(lat) * S / wall / 1e9, 3),
-                         "p50_ms": round(float(np.percentile(lat_ms, 50)), 2),
-                         "p99_ms": round(float(np.percentile(lat_ms, 99)), 2)}
-        # CPU proxy at the same concurrency (one file per thread, bounded sample)
+            p = subprocess.run([tool, str(C), str(args.client_seconds), kind, str(S), str(N), "500", "3"],
+                               capture_output=True, text=True, timeout=300)
+            if p.returncode != 0:
+                raise LegError(f"batcher_load {C} {kind}: rc {p.returncode}: {p.stderr[-300:]}")
+            r = json.loads(p.stdout.strip().splitlines()[-1])
+            ok &= r["ok"] and [r["file0_id"], r["file1_id"]] == want
+            row[kind] = {k: r[k] for k in ("requests", "gbps", "p50_ms", "p99_ms")}
+            st = r["stats"]
+            row[kind]["batches"] = st["batches"]
+            row[kind]["mean_batch"] = round(st["requests"] / max(st["batches"], 1), 1)
+            row[kind]["device_ms_per_batch"] = round(st["device_s"] / max(st["batches"], 1) * 1e3, 2)
         th_cpu = min(C, cores)
-        nf = max(th_cpu, int(th_cpu * 1.0 / 0.0012))  # ~1 s of work
+        nf = max(th_cpu, int(th_cpu / 0.0012))  # ~1 s of work
         secs, _, _ = O.cpu_upload_bench(nf, S, N, th_cpu, use_openssl=True)
         cpu = nf * S / secs / 1e9 if secs > 0 else None
-        if C == 1:
-            cpu_one = secs / nf if secs > 0 else None
+        if C == 1 and secs > 0:
+            cpu_one = secs / nf
         row["cpu_upload_gbps"] = round(cpu, 3) if cpu else None
         row["cpu_threads"] = th_cpu
-        if cpu_one:  # one connection handler's file, queued behind C / cores others
+        if cpu_one:  # one handler's file, queued behind C / threads others
             row["cpu_latency_est_ms"] = round(cpu_one * 1e3 * ((C + th_cpu - 1) // th_cpu), 2)
         rows.append(row)
-        log(f"batcher: {C} clients: upload {row['upload']['gbps']} GB/s p50 {row['upload']['p50_ms']} ms, "
-            f"download {row['download']['gbps']} GB/s; cpu {row['cpu_upload_gbps']} GB/s")
-    st = b.stats()
-    b.close()
+        log(f"batcher: {C} clients: upload {row['upload']['gbps']} GB/s p50 {row['upload']['p50_ms']} ms "
+            f"(batch {row['upload']['mean_batch']}, device {row['upload']['device_ms_per_batch']} ms), "
+            f"download {row['download']['gbps']} GB/s p50 {row['download']['p50_ms']} ms; cpu {row['cpu_upload_gbps']}")
     cross = next((r["clients"] for r in rows if r["cpu_upload_gbps"] and r["upload"]["gbps"] > r["cpu_upload_gbps"]),
                  None)
-    if not good[0]:
-        raise LegError("batcher leg: a client result differs from hashlib/base64")
-    return {"file_bytes": S, "nfrag": N, "rows": rows, "stats": st, "crossover_clients_upload": cross,
-            "ok": good[0], "cpu_cores": cores,
-            "note": "host buffers (each request crosses PCIe in and out); latency = one handler's blocking call; "
-                    "cpu = the oracle's C proxy with min(C, cores) threads (OpenSSL SHA-256 + scalar Base64), "
-                    "cpu_latency_est = one file's single-thread time x ceil(C / threads)"}
+    if not ok:
+        raise LegError("batcher leg: a client result is wrong")
+    return {"file_bytes": S, "nfrag": N, "rows": rows, "crossover_clients_upload": cross, "ok": ok,
+            "cpu_cores": cores,
+            "note": "native client threads (tools/batcher_load), host buffers: each request crosses PCIe in and "
+                    "out; latency = one handler's blocking call; cpu = the oracle's C proxy with min(C, cores) "
+                    "threads (OpenSSL SHA-256 + scalar Base64); cpu_latency_est = one file's single-thread time x "
+                    "ceil(C / threads)"}
 
 
 def long_leg(args):

@@ -17,11 +17,16 @@
 // out for uploads; Base64 in, file out for downloads): that, not the
 // kernels, bounds a host-buffer caller at high concurrency.
 //
-// Hand-off per request (all under the batcher mutex):
+// Hand-off per request:
 //   0 queued -> 1 worker assigned its staging slot (in_dst) -> 2 handler
 //   copied its input in (BatchSync::copied_in) -> 3 results ready (out_src,
 //   status) -> 4 handler copied its output out (BatchSync::copied_out); the
 //   worker reuses the staging only after every request of its batch did.
+// Locks: the batcher mutex guards only the queue and the stats (held for a
+// few instructions); a request's phase has its own mutex, shared by its
+// handler and the worker alone; a batch's counters have the BatchSync's.
+// Whoever publishes a phase notifies while holding that lock, so the other
+// side cannot see the phase, finish and free the object first.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,6 +40,7 @@
 #include <vector>
 
 #include "../../include/dfs_gpu.h"
+#include "dfs_internal.h"
 
 namespace {
 
@@ -45,13 +51,15 @@ uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
 struct Req;
 
 // Lives on the worker's stack for one batch.  Handlers only touch it (under
-// the batcher mutex) before their submit returns; the worker leaves the
-// batch only after `copied_out` reached the batch size, so it outlives
-// every use.  Requests themselves live on the handlers' stacks: the worker
-// never reads a request once its handler may have returned.
+// its mutex) before their submit returns; the worker leaves the batch only
+// after `copied_out` reached the batch size, so it outlives every use.
+// Requests themselves live on the handlers' stacks: the worker never reads
+// a request once its handler may have returned.
 struct BatchSync {
+    std::mutex mu;
     std::condition_variable cv;  // a handler advanced its request
     size_t copied_in = 0, copied_out = 0;
+    double return_s = 0;         // handlers' results-ready -> return time
 };
 
 enum Kind { kUpload = 0, kDownload = 1 };  // download kinds: 1 + (exp_frag ? 2 : 0) + (exp_file ? 1 : 0)
@@ -80,8 +88,16 @@ struct Req {
     uint8_t* in_dst = nullptr;         // staging slot of the input
     const uint8_t* out_src = nullptr;  // staging of the output
     int status = DFS_OK;
+    std::mutex mu;  // guards phase (and the fields the phase publishes)
     std::condition_variable cv;
 };
+
+// Publish phase `p` of request r (the worker side).
+void publish(Req* r, int p) {
+    std::lock_guard<std::mutex> lk(r->mu);
+    r->phase = p;
+    r->cv.notify_one();
+}
 
 struct Buf {
     void* p = nullptr;
@@ -89,7 +105,10 @@ struct Buf {
     bool pinned = false;
     int grow(size_t n) {
         if (n <= cap) return DFS_OK;
-        const size_t want = std::max<size_t>({n, cap + cap / 2, size_t(1) << 20});
+        // doubling from 64 MiB: a pinned allocation and the free of the old
+        // one are expensive (page pinning; frees synchronise the device)
+        size_t want = std::max<size_t>(cap, size_t(64) << 20);
+        while (want < n) want *= 2;
         void* q = nullptr;
         if ((pinned ? hipHostMalloc(&q, want, hipHostMallocDefault) : hipMalloc(&q, want)) != hipSuccess)
             return DFS_E_NOMEM;
@@ -109,6 +128,7 @@ struct Buf {
 struct Worker {
     dfs_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // blocking-sync event: the worker sleeps instead of spinning on the CPU share
     Buf pin_in, pin_out, d_in, d_out, d_dig;
     std::thread th;
     Worker() {
@@ -128,24 +148,35 @@ struct dfs_batcher {
     uint64_t q_bytes = 0;
     bool stop = false;
     std::vector<Worker*> workers;
-    uint64_t n_batches = 0, n_requests = 0, max_batch = 0;
+    dfs_batcher_stats_t st{};
 };
 
 namespace {
 
-// Give every request its staging slot and wait until all copied their input.
-void stage_in(dfs_batcher* B, std::vector<Req*>& batch, BatchSync& bs, uint8_t* base,
-              const std::vector<uint64_t>& off) {
-    std::unique_lock<std::mutex> lk(B->mu);
-    for (size_t i = 0; i < batch.size(); ++i) {
-        batch[i]->in_dst = base + off[i];
-        batch[i]->phase = 1;
-        batch[i]->cv.notify_one();
-    }
-    bs.cv.wait(lk, [&] { return bs.copied_in == batch.size(); });
+bool wait_stream(Worker& w) {
+    return hipEventRecord(w.done, w.stream) == hipSuccess && hipEventSynchronize(w.done) == hipSuccess;
 }
 
-int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs) {
+struct Timing {
+    double stage_in = 0, device = 0;
+};
+
+double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
+// Give every request its staging slot and wait until all copied their input.
+void stage_in(dfs_batcher* B, std::vector<Req*>& batch, BatchSync& bs, uint8_t* base,
+              const std::vector<uint64_t>& off, Timing& tm) {
+    const auto t0 = Clock::now();
+    for (size_t i = 0; i < batch.size(); ++i) {
+        batch[i]->in_dst = base + off[i];
+        publish(batch[i], 1);
+    }
+    std::unique_lock<std::mutex> lk(bs.mu);
+    bs.cv.wait(lk, [&] { return bs.copied_in == batch.size(); });
+    tm.stage_in = since(t0);
+}
+
+int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs, Timing& tm) {
     const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
     std::vector<dfs_span> spans(n);
     std::vector<uint64_t> in_off(n);
@@ -163,20 +194,25 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
     if (!rc) rc = w.d_out.grow(b64_total + 16);
     if (!rc) rc = w.d_dig.grow(dig_bytes);
     if (rc) return rc;
-    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off);
+    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off, tm);
+    const auto t_dev = Clock::now();
     std::vector<uint64_t> b64_off(static_cast<uint64_t>(n) * N + 1);
     uint8_t* d_fd = w.d_dig.as<uint8_t>();
     uint8_t* d_frd = d_fd + 32ull * n;
     if (total && hipMemcpyAsync(w.d_in.p, w.pin_in.p, total, hipMemcpyHostToDevice, w.stream) != hipSuccess)
         return DFS_E_HIP;
+    // one stream per worker (DFS_SERIAL: the Base64 kernel follows the SHA
+    // kernel on it): a box exposes few hardware queues (GPU_MAX_HW_QUEUES=4),
+    // and streams sharing one would serialise the workers' batches
     rc = dfs_upload_batch(w.ctx, w.d_in.as<uint8_t>(), spans.data(), n, N, d_fd, d_frd, w.d_out.as<char>(),
-                          b64_total, b64_off.data(), DFS_DEVICE_PTRS);
+                          b64_total, b64_off.data(), DFS_DEVICE_PTRS | DFS_SERIAL);
     if (rc) return rc;
     uint8_t* h = w.pin_out.as<uint8_t>();
     if (hipMemcpyAsync(h, d_fd, dig_bytes, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
         (b64_total && hipMemcpyAsync(h + dig_bytes, w.d_out.p, b64_total, hipMemcpyDeviceToHost, w.stream) != hipSuccess) ||
-        hipStreamSynchronize(w.stream) != hipSuccess)
+        !wait_stream(w))
         return DFS_E_HIP;
+    tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
         Req* r = batch[i];
         std::memcpy(r->fd, h + 32ull * i, 32);
@@ -186,7 +222,7 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
     return DFS_OK;
 }
 
-int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs) {
+int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs, Timing& tm) {
     const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
     const bool have_f = batch.front()->exp_frag != nullptr, have_i = batch.front()->exp_file != nullptr;
     std::vector<uint64_t> in_off(n), file_len(n), file_off(n);
@@ -219,7 +255,8 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
     if (!rc) rc = w.d_in.grow(total + 16);
     if (!rc) rc = w.d_out.grow(out_total + 16);
     if (rc) return rc;
-    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off);
+    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off, tm);
+    const auto t_dev = Clock::now();
     if (total && hipMemcpyAsync(w.d_in.p, w.pin_in.p, total, hipMemcpyHostToDevice, w.stream) != hipSuccess)
         return DFS_E_HIP;
     std::vector<int32_t> st(n);
@@ -229,8 +266,9 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
     if (rc != DFS_OK && rc != DFS_E_MISSING && rc != DFS_E_DECODE && rc != DFS_E_FRAG_MISMATCH && rc != DFS_E_CORRUPT)
         return rc;
     if (out_total && (hipMemcpyAsync(w.pin_out.p, w.d_out.p, out_total, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
-                      hipStreamSynchronize(w.stream) != hipSuccess))
+                      !wait_stream(w)))
         return DFS_E_HIP;
+    tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
         batch[i]->status = st[i];
         batch[i]->out_src = w.pin_out.as<uint8_t>() + file_off[i];
@@ -267,25 +305,35 @@ void worker_main(dfs_batcher* B, Worker* w) {
                 B->q_bytes -= r->need;
                 it = B->q.erase(it);
             }
-            ++B->n_batches;
-            B->n_requests += batch.size();
-            B->max_batch = std::max<uint64_t>(B->max_batch, batch.size());
+            const auto now = Clock::now();
+            ++B->st.batches;
+            B->st.requests += batch.size();
+            B->st.max_batch = std::max<uint64_t>(B->st.max_batch, batch.size());
+            for (Req* r : batch) B->st.queue_s += std::chrono::duration<double>(now - r->arrive).count();
             if (!B->q.empty()) B->cv_work.notify_one();
         }
-        const int rc = batch.front()->kind == kUpload ? run_uploads(B, *w, batch, bs) : run_downloads(B, *w, batch, bs);
+        Timing tm;
+        const int rc = batch.front()->kind == kUpload ? run_uploads(B, *w, batch, bs, tm) : run_downloads(B, *w, batch, bs, tm);
+        const auto t_done = Clock::now();
         // Results ready (or the batch failed); reuse the staging only after
         // every handler copied its output out.
-        std::unique_lock<std::mutex> lk(B->mu);
         for (Req* r : batch) {
             if (rc != DFS_OK) {
                 r->status = rc;
                 r->out_src = nullptr;
             }
-            r->phase = 3;
-            r->cv.notify_one();
+            publish(r, 3);
         }
         const size_t n = batch.size();
-        bs.cv.wait(lk, [&] { return bs.copied_out == n; });
+        {
+            std::unique_lock<std::mutex> lk(bs.mu);
+            bs.cv.wait(lk, [&] { return bs.copied_out == n; });
+        }
+        std::lock_guard<std::mutex> lk(B->mu);
+        B->st.stage_in_s += tm.stage_in;
+        B->st.device_s += tm.device;
+        B->st.stage_out_s += std::chrono::duration<double>(Clock::now() - t_done).count();
+        B->st.return_s += bs.return_s;
     }
 }
 
@@ -293,12 +341,17 @@ void worker_main(dfs_batcher* B, Worker* w) {
 // staging slot when the worker hands it out, wait for the results, copy the
 // output out of the staging.
 int submit(dfs_batcher* B, Req& r) {
-    r.arrive = Clock::now();
-    std::unique_lock<std::mutex> lk(B->mu);
-    if (B->stop) return DFS_E_ARG;
-    B->q.push_back(&r);
-    B->q_bytes += r.need;
-    B->cv_work.notify_one();
+    const auto t_call = Clock::now();
+    {
+        std::lock_guard<std::mutex> lk(B->mu);
+        if (B->stop) return DFS_E_ARG;
+        r.arrive = Clock::now();
+        B->st.enqueue_s += std::chrono::duration<double>(r.arrive - t_call).count();
+        B->q.push_back(&r);
+        B->q_bytes += r.need;
+        B->cv_work.notify_one();
+    }
+    std::unique_lock<std::mutex> lk(r.mu);
     r.cv.wait(lk, [&] { return r.phase >= 1; });
     if (r.phase == 1) {
         lk.unlock();
@@ -313,19 +366,21 @@ int submit(dfs_batcher* B, Req& r) {
                 d += s.len;
             }
         }
+        {
+            std::lock_guard<std::mutex> bl(r.sync->mu);
+            ++r.sync->copied_in;
+            r.sync->cv.notify_one();
+        }
         lk.lock();
-        r.phase = 2;
-        ++r.sync->copied_in;
-        r.sync->cv.notify_one();
     }
     r.cv.wait(lk, [&] { return r.phase >= 3; });
-    if (r.out_src && r.out_bytes && (r.kind == kUpload || r.status == DFS_OK)) {
-        lk.unlock();
+    lk.unlock();
+    const auto t_ready = Clock::now();
+    if (r.out_src && r.out_bytes && (r.kind == kUpload || r.status == DFS_OK))
         std::memcpy(r.kind == kUpload ? static_cast<void*>(r.b64) : static_cast<void*>(r.out), r.out_src, r.out_bytes);
-        lk.lock();
-    }
-    r.phase = 4;
     const int status = r.status;
+    std::lock_guard<std::mutex> bl(r.sync->mu);  // the last touch of the batch (the worker waits for it)
+    r.sync->return_s += std::chrono::duration<double>(Clock::now() - t_ready).count();
     ++r.sync->copied_out;
     r.sync->cv.notify_one();
     return status;
@@ -358,8 +413,9 @@ int dfs_batcher_create(int device, uint32_t nfrag, const dfs_batcher_opts* opts,
         }
         B->workers.push_back(w);
         rc = dfs_open(&w->ctx, device);
-        if (rc == DFS_OK && hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) rc = DFS_E_HIP;
-        if (rc == DFS_OK) rc = dfs_set_stream(w->ctx, w->stream);
+        if (rc == DFS_OK) w->stream = dfs::ctx_stream(w->ctx);  // the ctx's own stream: one hardware queue per worker
+        if (rc == DFS_OK && hipEventCreateWithFlags(&w->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
+            rc = DFS_E_HIP;
     }
     if (rc == DFS_OK)
         for (Worker* w : B->workers) w->th = std::thread(worker_main, B, w);
@@ -382,20 +438,18 @@ int dfs_batcher_destroy(dfs_batcher* B) {
         if (w->th.joinable()) w->th.join();
         (void)hipSetDevice(B->device);
         for (Buf* b : {&w->pin_in, &w->pin_out, &w->d_in, &w->d_out, &w->d_dig}) b->release();
-        if (w->ctx) dfs_close(w->ctx);
-        if (w->stream) (void)hipStreamDestroy(w->stream);
+        if (w->ctx) dfs_close(w->ctx);  // destroys its stream
+        if (w->done) (void)hipEventDestroy(w->done);
         delete w;
     }
     delete B;
     return DFS_OK;
 }
 
-int dfs_batcher_stats(dfs_batcher* B, uint64_t* batches, uint64_t* requests, uint64_t* max_batch) {
-    if (!B) return DFS_E_ARG;
+int dfs_batcher_stats(dfs_batcher* B, dfs_batcher_stats_t* out) {
+    if (!B || !out) return DFS_E_ARG;
     std::lock_guard<std::mutex> lk(B->mu);
-    if (batches) *batches = B->n_batches;
-    if (requests) *requests = B->n_requests;
-    if (max_batch) *max_batch = B->max_batch;
+    *out = B->st;
     return DFS_OK;
 }
 

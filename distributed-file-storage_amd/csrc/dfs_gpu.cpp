@@ -59,7 +59,9 @@ enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_S
 struct dfs_ctx {
     int device = 0;
     hipStream_t own = nullptr;   // default stream of this ctx
-    hipStream_t aux = nullptr;   // second stream (Base64 beside SHA)
+    hipStream_t aux = nullptr;   // second stream (Base64 beside SHA), created on first use: a
+                                 // process has few hardware queues (GPU_MAX_HW_QUEUES=4 on the
+                                 // box) and every stream takes one until they are shared
     hipStream_t user = nullptr;  // borrowed (dfs_set_stream)
     bool profiling = false;
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
@@ -76,6 +78,17 @@ struct dfs_ctx {
     // launch that used them) so it cannot overwrite descriptors in flight.
     hipEvent_t scratch_ev = nullptr;
     hipStream_t scratch_stream = nullptr;
+    // Pinned staging for the host -> device descriptor copies of one call
+    // (two arenas, alternating per call): an async copy from pageable memory
+    // is staged by the runtime and blocks, so tables go through here.  An
+    // arena is reused once the copies of the call before last completed.
+    struct Arena {
+        uint8_t* p = nullptr;
+        size_t cap = 0, used = 0;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    } arena[2];
+    int cur_arena = 0;
     DevBuf buf[B_COUNT];
     dfs::StoreStaging* store = nullptr;  // pinned staging ring of the fragment store
     std::mutex mu;
@@ -222,15 +235,41 @@ struct Scratch {
     hipStream_t s;
     Scratch(dfs_ctx* ctx, hipStream_t st) : c(ctx), s(st) {
         if (c->scratch_stream && c->scratch_stream != s) (void)hipStreamWaitEvent(s, c->scratch_ev, 0);
+        c->cur_arena ^= 1;
+        auto& a = c->arena[c->cur_arena];
+        if (a.pending) (void)hipEventSynchronize(a.ev);
+        a.pending = false;
+        a.used = 0;
     }
     ~Scratch() {
         if (hipEventRecord(c->scratch_ev, s) == hipSuccess) c->scratch_stream = s;
+        auto& a = c->arena[c->cur_arena];
+        if (a.used && hipEventRecord(a.ev, s) == hipSuccess) a.pending = true;
     }
 };
 
+constexpr size_t kArenaMax = 64ull << 20;  // larger host buffers (file data) are copied directly
+
 int put(dfs_ctx* c, int id, const void* src, size_t n, hipStream_t s) {
     HIPC(c->buf[id].ensure(n));
-    if (n) HIPC(hipMemcpyAsync(c->buf[id].p, src, n, hipMemcpyHostToDevice, s));
+    if (!n) return DFS_OK;
+    auto& a = c->arena[c->cur_arena];
+    if (n <= kArenaMax) {
+        if (a.used + n > a.cap) {
+            if (a.used) HIPC(hipStreamSynchronize(s));  // this call's earlier copies still read the arena
+            const size_t want = std::max<size_t>({a.used + n, 2 * a.cap, size_t(1) << 20});
+            if (a.p) (void)hipHostFree(a.p);
+            a.p = nullptr;
+            a.cap = a.used = 0;
+            HIPC(hipHostMalloc(reinterpret_cast<void**>(&a.p), want, hipHostMallocDefault));
+            a.cap = want;
+        }
+        std::memcpy(a.p + a.used, src, n);
+        HIPC(hipMemcpyAsync(c->buf[id].p, a.p + a.used, n, hipMemcpyHostToDevice, s));
+        a.used += (n + 255) & ~size_t(255);
+        return DFS_OK;
+    }
+    HIPC(hipMemcpyAsync(c->buf[id].p, src, n, hipMemcpyHostToDevice, s));
     return DFS_OK;
 }
 
@@ -290,11 +329,12 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
     for (int i = 0; e == hipSuccess && i < 2 * DFS_T_COUNT; ++i) e = hipEventCreate(&c->ev[i]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming);
+    for (auto& a : c->arena)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&a.ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         dfs_close(c);
         return hip_fail(e, "dfs_open");
@@ -314,6 +354,10 @@ int dfs_close(dfs_ctx* c) {
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : {c->fork, c->join, c->scratch_ev})
         if (ev) (void)hipEventDestroy(ev);
+    for (auto& a : c->arena) {
+        if (a.ev) (void)hipEventDestroy(a.ev);
+        if (a.p) (void)hipHostFree(a.p);
+    }
     if (c->own) (void)hipStreamDestroy(c->own);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     delete c;
@@ -829,7 +873,7 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     if (!d_frd || (do_fileid && !d_fd) || (do_b64 && !d_b64)) return DFS_E_ARG;
     if (do_b64 && (reinterpret_cast<uintptr_t>(d_b64) & 3u)) return DFS_E_ARG;
     hipStream_t s = c->stream();
-    Scratch scratch(c, s);
+    
     if (flags & DFS_B64_ONLY) {  // the HBM-bound encode pass alone
         if (!do_b64) return DFS_OK;
         Timer tb(c);
@@ -840,6 +884,7 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
         tb.end(DFS_T_TOTAL, s);
         return DFS_OK;
     }
+    if (!serial && !c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     hipStream_t sb = serial ? s : c->aux;
     Timer tm(c);
     const bool two = do_b64 && !fused;  // separate Base64 encode kernel
@@ -880,6 +925,7 @@ int dfs_upload_plan_run(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, 
     if (!c || !p || p->device != c->device) return DFS_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = enter(c)) return rc;
+    Scratch scratch(c, c->stream());
     return run_plan_locked(c, p, d_files, d_fd, d_frd, d_b64, flags);
 }
 

@@ -52,6 +52,12 @@ class dfs_span(ctypes.Structure):
     _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint64)]
 
 
+class dfs_batcher_stats_t(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("max_batch", ctypes.c_uint64),
+                ("queue_s", ctypes.c_double), ("stage_in_s", ctypes.c_double), ("device_s", ctypes.c_double),
+                ("stage_out_s", ctypes.c_double), ("enqueue_s", ctypes.c_double), ("return_s", ctypes.c_double)]
+
+
 class dfs_batcher_opts(ctypes.Structure):
     _fields_ = [("max_wait_us", ctypes.c_uint32), ("max_files", ctypes.c_uint32), ("max_bytes", ctypes.c_uint64),
                 ("depth", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
@@ -104,7 +110,7 @@ SIGNATURES = {
     "dfs_store_read_fragments": (_int, [_vp, ctypes.c_char_p, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _u32]),
     "dfs_batcher_create": (_int, [_int, _u32, _vp, ctypes.POINTER(_vp)]),
     "dfs_batcher_destroy": (_int, [_vp]),
-    "dfs_batcher_stats": (_int, [_vp, _vp, _vp, _vp]),
+    "dfs_batcher_stats": (_int, [_vp, _vp]),
     "dfs_submit_upload": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
     "dfs_submit_download": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "dfs_comm_unique_id": (_int, [_vp]),

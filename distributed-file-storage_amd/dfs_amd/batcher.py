@@ -67,9 +67,9 @@ class Batcher:
         return st, (out[:file_len].tobytes() if st == 0 else None)
 
     def stats(self) -> dict:
-        b, r, m = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-        check(lib().dfs_batcher_stats(self._b, ctypes.byref(b), ctypes.byref(r), ctypes.byref(m)), "dfs_batcher_stats")
-        return {"batches": b.value, "requests": r.value, "max_batch": m.value}
+        st = L.dfs_batcher_stats_t()
+        check(lib().dfs_batcher_stats(self._b, ctypes.byref(st)), "dfs_batcher_stats")
+        return {k: getattr(st, k) for k, _ in L.dfs_batcher_stats_t._fields_}
 
     def close(self) -> None:
         if self._b:

@@ -356,7 +356,16 @@ typedef struct dfs_batcher_opts {
 int dfs_batcher_create(int device, uint32_t nfrag, const dfs_batcher_opts* opts, dfs_batcher** batcher);
 /* Stops accepting requests, finishes the queued ones, joins the workers. */
 int dfs_batcher_destroy(dfs_batcher* batcher);
-int dfs_batcher_stats(dfs_batcher* batcher, uint64_t* batches, uint64_t* requests, uint64_t* max_batch);
+typedef struct dfs_batcher_stats_t {
+    uint64_t batches, requests, max_batch;
+    double queue_s;      /* requests' time from submit to a worker taking them (summed) */
+    double stage_in_s;   /* workers waiting for handlers to copy inputs in       */
+    double device_s;     /* H2D + kernels + D2H per batch                        */
+    double stage_out_s;  /* workers waiting for handlers to copy outputs out     */
+    double enqueue_s;    /* handlers' time from the call to holding a queue slot */
+    double return_s;     /* handlers' time from results ready to returning       */
+} dfs_batcher_stats_t;
+int dfs_batcher_stats(dfs_batcher* batcher, dfs_batcher_stats_t* stats);
 /* One upload (SN:127, 138-159, 636): file_digest[32], frag_digest[nfrag*32],
  * the fragments' Base64 back to back in b64 (b64_off[nfrag+1], relative). */
 int dfs_submit_upload(dfs_batcher* batcher, const uint8_t* file, uint64_t len, uint8_t* file_digest,

@@ -1,0 +1,175 @@
+// batcher_load.cpp — closed-loop load generator for the request batcher.
+//
+// C native threads stand for StorageNode's connection handlers
+// (StorageNode.java:28-31): each submits one file at a time through
+// dfs_submit_upload or dfs_submit_download (host buffers) until the deadline
+// and records every call's latency.  Native threads, so the measurement
+// carries no interpreter lock.  Prints one JSON line; bench.py runs it per
+// concurrency and checks the printed fileIds against its own checker.
+//
+//   batcher_load <clients> <seconds> <upload|download> <file_bytes> <nfrag> [max_wait_us] [depth]
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/dfs_gpu.h"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+constexpr int kDistinct = 64;
+constexpr uint64_t kSeed = 0x5EED5EEDull;
+
+uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+// The bench's synthetic file f (dfs_synth_fill's byte stream).
+void synth(uint64_t f, uint64_t len, uint8_t* out) {
+    for (uint64_t o = 0; o < len; o += 8) {
+        const uint64_t v = splitmix64(kSeed ^ ((f << 40) | (o >> 3)));
+        for (uint64_t b = 0; b < 8 && o + b < len; ++b) out[o + b] = static_cast<uint8_t>(v >> (8 * b));
+    }
+}
+
+std::string hex(const uint8_t* d) {
+    static const char* k = "0123456789abcdef";
+    std::string s(64, '0');
+    for (int i = 0; i < 32; ++i) {
+        s[2 * i] = k[d[i] >> 4];
+        s[2 * i + 1] = k[d[i] & 15];
+    }
+    return s;
+}
+
+uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
+
+// cgroup v2 CPU accounting of this process's share (a GPU box gives a
+// process a CPU quota): usage and throttled microseconds.
+void cpu_stat(unsigned long long& usage, unsigned long long& throttled) {
+    usage = throttled = 0;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.stat", "r")) {
+        char key[64];
+        unsigned long long v;
+        while (std::fscanf(f, "%63s %llu", key, &v) == 2) {
+            if (!std::strcmp(key, "usage_usec")) usage = v;
+            if (!std::strcmp(key, "throttled_usec")) throttled = v;
+        }
+        std::fclose(f);
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 6) {
+        std::fprintf(stderr, "usage: %s clients seconds upload|download file_bytes nfrag [max_wait_us] [depth]\n", argv[0]);
+        return 2;
+    }
+    const int C = std::atoi(argv[1]);
+    const double secs = std::atof(argv[2]);
+    const bool up = std::strcmp(argv[3], "upload") == 0;
+    const uint64_t S = std::strtoull(argv[4], nullptr, 10);
+    const uint32_t N = static_cast<uint32_t>(std::atoi(argv[5]));
+    dfs_batcher_opts o{};
+    if (argc > 6) o.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
+    if (argc > 7) o.depth = static_cast<uint32_t>(std::atoi(argv[7]));
+    if (C < 1 || N < 1 || N > 64) return 2;
+    dfs_batcher* B = nullptr;
+    if (int rc = dfs_batcher_create(0, N, &o, &B)) {
+        std::fprintf(stderr, "dfs_batcher_create: %s\n", dfs_strerror(rc));
+        return 3;
+    }
+    // distinct files, their upload results (Base64, digests) for the download clients
+    std::vector<std::vector<uint8_t>> file(kDistinct, std::vector<uint8_t>(S));
+    std::vector<std::vector<uint8_t>> fd(kDistinct, std::vector<uint8_t>(32)), frd(kDistinct, std::vector<uint8_t>(32 * N));
+    std::vector<std::vector<char>> b64(kDistinct);
+    std::vector<std::vector<uint64_t>> off(kDistinct, std::vector<uint64_t>(N + 1));
+    const uint64_t cap = N * enc_len(S / N + 1) + 16;
+    for (int f = 0; f < kDistinct; ++f) {
+        synth(f, S, file[f].data());
+        b64[f].resize(cap);
+        if (int rc = dfs_submit_upload(B, file[f].data(), S, fd[f].data(), frd[f].data(), b64[f].data(), cap,
+                                       off[f].data())) {
+            std::fprintf(stderr, "warm-up upload: %s\n", dfs_strerror(rc));
+            return 3;
+        }
+    }
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false}, bad{false};
+    std::vector<std::vector<double>> lat(C);
+    Clock::time_point deadline, measure_from;
+    std::vector<std::thread> th;
+    th.reserve(C);
+    for (int t = 0; t < C; ++t) {
+        th.emplace_back([&, t] {
+            const int f = t % kDistinct;
+            std::vector<uint8_t> mfd(32), mfrd(32 * N), out(up ? 1 : S);
+            std::vector<char> mb(up ? cap : 1);
+            std::vector<uint64_t> moff(N + 1);
+            std::vector<dfs_span> spans(N);
+            for (uint32_t k = 0; k < N; ++k) spans[k] = dfs_span{off[f][k], off[f][k + 1] - off[f][k]};
+            ++ready;
+            while (!go.load()) std::this_thread::yield();
+            for (uint64_t it = 0;; ++it) {
+                const auto t0 = Clock::now();
+                int rc;
+                if (up) {
+                    rc = dfs_submit_upload(B, file[f].data(), S, mfd.data(), mfrd.data(), mb.data(), cap, moff.data());
+                } else {
+                    rc = dfs_submit_download(B, b64[f].data(), spans.data(), S, frd[f].data(), fd[f].data(), out.data());
+                }
+                const auto t1 = Clock::now();
+                if (t0 >= measure_from) lat[t].push_back(std::chrono::duration<double>(t1 - t0).count());
+                if (rc != DFS_OK) bad = true;
+                else if (it % 8) {  // every 8th result is compared in full (the handler's own work stays small)
+                } else if (up && (std::memcmp(mfd.data(), fd[f].data(), 32) || std::memcmp(mfrd.data(), frd[f].data(), 32 * N) ||
+                                std::memcmp(mb.data(), b64[f].data(), off[f][N])))
+                    bad = true;
+                else if (!up && std::memcmp(out.data(), file[f].data(), S))
+                    bad = true;
+                if (t1 >= deadline) break;
+            }
+        });
+    }
+    while (ready.load() < C) std::this_thread::yield();
+    // 0.5 s of warm-up at the same concurrency (staging buffers reach their
+    // size), then the measured window: requests started inside it
+    const auto dur = [](double x) { return std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(x)); };
+    measure_from = Clock::now() + dur(0.5);
+    deadline = measure_from + dur(secs);
+    go = true;
+    std::this_thread::sleep_until(measure_from);
+    unsigned long long u0, th0, u1, th1;
+    cpu_stat(u0, th0);
+    const auto t0 = Clock::now();
+    for (auto& x : th) x.join();
+    const double wall = std::chrono::duration<double>(deadline - t0).count();
+    cpu_stat(u1, th1);
+    std::vector<double> all;
+    for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+    std::sort(all.begin(), all.end());
+    auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, static_cast<size_t>(p * all.size()))]; };
+    dfs_batcher_stats_t st{};
+    dfs_batcher_stats(B, &st);
+    dfs_batcher_destroy(B);
+    std::printf("{\"clients\": %d, \"kind\": \"%s\", \"requests\": %zu, \"wall_s\": %.4f, \"gbps\": %.4f, "
+                "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"cpu_s\": %.3f, \"throttled_s\": %.3f, \"ok\": %s, \"file0_id\": \"%s\", \"file1_id\": \"%s\", "
+                "\"stats\": {\"batches\": %llu, \"requests\": %llu, \"max_batch\": %llu, \"queue_s\": %.4f, "
+                "\"stage_in_s\": %.4f, \"device_s\": %.4f, \"stage_out_s\": %.4f, \"enqueue_s\": %.4f, \"return_s\": %.4f}}\n",
+                C, up ? "upload" : "download", all.size(), wall, all.size() * static_cast<double>(S) / wall / 1e9,
+                pct(0.5) * 1e3, pct(0.99) * 1e3, (u1 - u0) / 1e6, (th1 - th0) / 1e6, bad ? "false" : "true", hex(fd[0].data()).c_str(),
+                hex(fd[1].data()).c_str(), (unsigned long long)st.batches, (unsigned long long)st.requests,
+                (unsigned long long)st.max_batch, st.queue_s, st.stage_in_s, st.device_s, st.stage_out_s, st.enqueue_s,
+                st.return_s);
+    return bad ? 1 : 0;
+}
