@@ -46,6 +46,10 @@ struct StreamJob {
 
 constexpr int kShaBlock = 256;       // threads per SHA workgroup (4 waves)
 constexpr size_t kShaQueueBytes = 4 * (64 + 8192);  // SHA queue words + per-SIMD tokens
+// Launches of at most this many lanes (512 two-wave workgroups: all resident
+// at once) run the latency kernel sha256_chain; larger ones the persistent
+// throughput kernel sha256_lanes.
+constexpr uint32_t kChainMaxLanes = 32768;
 constexpr int kStreamBlock = 256;    // threads per stream workgroup
 constexpr int kEncPer = 4;           // encode: 12-byte groups per thread per tile
 constexpr int kDecGpl = 8;           // decode: 4-unit groups per thread per tile
@@ -107,9 +111,11 @@ struct BodyParse {
 };
 
 // Launchers (return hipError_t of the launch).
-// Persistent multi-message SHA-256.  `queue` is kShaQueueBytes of device
-// memory, zeroed by the launcher on `s` before the launch; the grid holds waves_per_simd waves
-// on each of the 1024 SIMDs (fewer for small batches).
+// Multi-message SHA-256: up to kChainMaxLanes lanes (without fused Base64)
+// the owner/helper latency kernel, else the persistent throughput kernel.
+// `queue` is kShaQueueBytes of device memory, zeroed by the launcher on `s`
+// before a persistent launch; its grid holds waves_per_simd waves on each of
+// the 1024 SIMDs (fewer for small batches).
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
                          int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr);

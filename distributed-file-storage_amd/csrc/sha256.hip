@@ -521,6 +521,137 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
     }
 }
 
+// ---------------------------------------------------------------------------
+// Latency kernel for launches too small to fill the chip (a batcher batch,
+// the long-fragment skew config, small host calls): each message's chain is
+// the critical path, and one wave issues every instruction of its lanes'
+// blocks.  Two waves share the 64 messages of a workgroup: the helper wave
+// (wave 1) loads each block, byte-swaps it, expands the message schedule and
+// writes K[t] + W[t] for all 64 rounds to LDS one block ahead; the owner
+// wave (wave 0) runs only the rounds (14 VALU ops each, K and W folded into
+// one LDS operand) — about 0.65 of the single-wave instruction stream of
+// sha256_lanes per block.  One workgroup barrier per block hands the two
+// LDS slots over (double buffering).  Lanes past their own block count keep
+// their state (predicated update); partial / resumed messages as in
+// sha256_lanes (kShaPartial stores the state, kShaResume loads it).
+constexpr int kChainBlock = 128;  // owner + helper wave
+
+__device__ __forceinline__ void owner_block(uint32_t (&st)[8], const uint4* __restrict__ kw, bool act) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    uint4 q = kw[0];
+#pragma unroll
+    for (int t4 = 0; t4 < 16; ++t4) {
+        const uint4 cur = q;
+        if (t4 + 1 < 16) q = kw[(t4 + 1) * 64];  // next quad of K+W in flight
+        const uint32_t v[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t tmp = h + ch(e, f, g) + v[j];
+            const uint32_t t1 = tmp + bsig1(e);
+            const uint32_t na = t1 + bsig0(a) + maj(a, b, c);
+            h = g; g = f; f = e; e = d + t1;
+            d = c; c = b; b = a; a = na;
+            asm volatile("" : "+v"(a), "+v"(e));
+        }
+    }
+    if (act) {
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+        st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    }
+}
+
+// K[t] + W[t] of block k of m (raw words r + look-ahead x for full blocks,
+// the padded tail for k < nb, zeros past the lane's own blocks) into
+// kw[t/4 * 64][t%4].
+__device__ __forceinline__ void helper_block(const Msg& m, uint32_t nb, uint32_t k, uint32_t (&r)[16], uint32_t x,
+                                             uint4* __restrict__ kw) {
+    uint32_t W[16];
+    if (k < m.nfull) {
+        to_be(r, x, m.sel);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) W[i] = r[i];
+    } else if (k < nb) {
+        tail_block(m, k - m.nfull, W);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) W[i] = 0u;
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+        if (t >= 16) {
+            W[t & 15] += ssig1(W[(t - 2) & 15]) + W[(t - 7) & 15] + ssig0(W[(t - 15) & 15]);
+            asm volatile("" : "+v"(W[t & 15]));
+        }
+        o[t & 3] = kK[t] + W[t & 15];
+        if ((t & 3) == 3) kw[(t >> 2) * 64] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+__global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __restrict__ base,
+                                                            const ShaDesc* __restrict__ descs, uint32_t n,
+                                                            uint32_t split, uint8_t* __restrict__ out0,
+                                                            uint8_t* __restrict__ out1, uint32_t* __restrict__ state) {
+    __shared__ uint4 kw[2][16 * 64];  // [slot][t/4][lane]: 32 KiB
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool owner = threadIdx.x < 64u;
+    const uint32_t gid = blockIdx.x * 64u + lane;
+    const bool live = gid < n;
+    Msg m{};
+    uint32_t nb = 0;
+    if (live) {
+        m = msg_setup(base, descs[gid]);
+        nb = m.nfull + ((m.flags & kShaPartial) ? 0u : m.ntb);
+    }
+    // same count in both waves: they read the same descriptors
+    const uint32_t kmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
+    if (owner) {
+        uint32_t st[8];
+        if (live && (m.flags & kShaResume)) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(state + 8ull * m.out);
+            const uint4 s0 = s4[0], s1 = s4[1];
+            st[0] = s0.x; st[1] = s0.y; st[2] = s0.z; st[3] = s0.w;
+            st[4] = s1.x; st[5] = s1.y; st[6] = s1.z; st[7] = s1.w;
+        } else {
+            init_state(st);
+        }
+        __syncthreads();  // block 0 staged
+        for (uint32_t k = 0; k < kmax; ++k) {
+            owner_block(st, kw[k & 1u] + lane, k < nb);
+            __syncthreads();
+        }
+        if (live) {
+            if (m.flags & kShaPartial) {
+                uint4* s4 = reinterpret_cast<uint4*>(state + 8ull * m.out);
+                s4[0] = make_uint4(st[0], st[1], st[2], st[3]);
+                s4[1] = make_uint4(st[4], st[5], st[6], st[7]);
+            } else {
+                store_digest(st, m.out, split, out0, out1);
+            }
+        }
+    } else {
+        // raw blocks k+1 (R) and k+2 (Q) in flight while block k+1 is expanded
+        const uint32_t* bp = (live && m.nfull) ? m.p : g_dummy_block;
+        const uint32_t last = (live && m.nfull) ? m.nfull - 1u : 0u;
+        const uint32_t sh = live ? m.sh : 0u;
+        uint32_t R[16], Q[16], xr, xq;
+        load_block(bp, sh, R, xr);
+        if (kmax) helper_block(m, nb, 0, R, xr, kw[0] + lane);
+        load_block(bp + 16u * min(1u, last), sh, R, xr);
+        __syncthreads();
+        for (uint32_t k = 0; k < kmax; ++k) {
+            if (k + 1 < kmax) {
+                load_block(bp + 16u * min(k + 2u, last), sh, Q, xq);
+                helper_block(m, nb, k + 1, R, xr, kw[(k + 1) & 1u] + lane);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) R[i] = Q[i];
+                xr = xq;
+            }
+            __syncthreads();
+        }
+    }
+}
+
 #define DFS_SHA_ARGS                                                                                     \
     const uint8_t *__restrict__ base, const ShaDesc *__restrict__ descs, uint32_t n, uint32_t split,       \
         uint32_t n_long, uint32_t cap, uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,             \
@@ -543,6 +674,11 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
                          hipStream_t s, uint32_t* state, char* b64) {
     if (n == 0) return hipSuccess;
+    if (!b64 && n <= kChainMaxLanes) {  // latency-bound launch: owner + helper waves
+        hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, split, out0,
+                           out1, state);
+        return hipGetLastError();
+    }
     hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
     if (e != hipSuccess) return e;
     const uint32_t n_long = (prio_lanes + 63u) / 64u;

@@ -608,3 +608,27 @@ def test_concurrent_handlers_share_one_ctx(engine):
         t.join(timeout=120)
     assert not errors, errors[0]
     assert not any(t.is_alive() for t in threads)
+
+
+def test_sha256_both_kernels_large_and_small_launches(engine):
+    """Launches up to dfs::kChainMaxLanes lanes run the owner/helper latency
+    kernel, larger ones the persistent throughput kernel: the same random
+    messages (every alignment, lengths around the padding boundaries) through
+    both, against hashlib."""
+    rng = np.random.default_rng(77)
+    n_big = 33000  # > kChainMaxLanes (32768)
+    lens = rng.integers(0, 700, n_big)
+    lens[:64] = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 129] + list(range(191, 242))
+    buf = rng.integers(0, 256, int(lens.sum()) + 8 * n_big, dtype=np.uint8)
+    offs, o = [], 0
+    for i, ln in enumerate(lens):
+        o += i % 4  # every alignment
+        offs.append(o)
+        o += int(ln)
+    spans = np.stack([np.array(offs, np.uint64), lens.astype(np.uint64)], axis=1)
+    raw = buf.tobytes()
+    want = [hashlib.sha256(raw[a:a + int(n)]).digest() for a, n in spans]
+    big = engine.sha256_spans(buf, spans)
+    assert all(big[i].tobytes() == want[i] for i in range(n_big))
+    small = engine.sha256_spans(buf, spans[:5000])
+    assert all(small[i].tobytes() == want[i] for i in range(5000))
