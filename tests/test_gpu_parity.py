@@ -632,3 +632,39 @@ def test_sha256_both_kernels_large_and_small_launches(engine):
     assert all(big[i].tobytes() == want[i] for i in range(n_big))
     small = engine.sha256_spans(buf, spans[:5000])
     assert all(small[i].tobytes() == want[i] for i in range(5000))
+
+
+def test_download_overlapped_large_batch(engine):
+    """Batches above dfs::kChainMaxLanes SHA lanes overlap the Base64 decode
+    (file order, progress counters) with the persistent SHA kernel, whose
+    lanes wait for their file's decode.  6,000 files (36,000 lanes): every
+    file rebuilt and verified, plus the failure statuses on a few files —
+    missing fragment (SN:443-446), invalid Base64 (SN:281), wrong fragment
+    digest (SN:250-257), wrong fileId (SN:455-458) — and their neighbours
+    unaffected."""
+    import base64
+    rng = np.random.default_rng(31)
+    nfiles, nfrag = 6000, 5
+    sizes = rng.integers(0, 20000, nfiles)
+    sizes[:7] = [0, 1, 2, 4, 5, 6, 7]
+    files = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in sizes]
+    texts, frag_h, file_h = [], [], []
+    for d in files:
+        parts = [d[o:o + n] for o, n in O.c_split(len(d), nfrag)]
+        texts.append([base64.b64encode(p) for p in parts])
+        frag_h.append([hashlib.sha256(p).hexdigest() for p in parts])
+        file_h.append(hashlib.sha256(d).hexdigest())
+    want = [0] * nfiles
+    texts[100][2] = None
+    want[100] = dfs_amd.DFS_E_MISSING
+    t = bytearray(texts[2000][1]); t[3] = ord("!"); texts[2000][1] = bytes(t)
+    want[2000] = dfs_amd.DFS_E_DECODE
+    frag_h[3000] = list(frag_h[3000]); frag_h[3000][4] = "0" * 64
+    want[3000] = dfs_amd.DFS_E_FRAG_MISMATCH
+    file_h[5999] = "f" * 64
+    want[5999] = dfs_amd.DFS_E_CORRUPT
+    res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+    for f, (st, body) in enumerate(res):
+        assert st == want[f], (f, st, want[f])
+        if want[f] == 0:
+            assert body == files[f], f
