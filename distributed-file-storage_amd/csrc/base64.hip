@@ -274,18 +274,12 @@ __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const 
 // each with one dwordx4 store at a 16-byte aligned address (a wave writes
 // 1 KiB contiguous per instruction).  Head, tail and final unit: dec_tail,
 // on wave 0 of the message's last tile.  Loads and stores are non-temporal.
-// ORDERED (the download beside the SHA kernel): tiles are taken grid-stride
-// (the whole grid sweeps the batch front to back, so files finish decoding
-// in order) and after each tile done[job.aux] (the job's file) is bumped
-// with agent-scope release: the SHA lanes of that file wait for it.
-template <bool ORDERED>
 __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
                                                                   const StreamJob* __restrict__ jobs,
                                                                   uint32_t njobs, uint64_t ntiles,
                                                                   uint8_t* __restrict__ out,
                                                                   int32_t* __restrict__ status,
-                                                                  uint64_t* __restrict__ out_len,
-                                                                  uint32_t* __restrict__ done) {
+                                                                  uint64_t* __restrict__ out_len) {
     constexpr int GPL = kDecGpl;
     constexpr uint32_t kGroups = GPL * kStreamBlock;  // 4-unit groups per tile
     constexpr uint32_t kChunks = 3 * GPL * 64;        // 16-byte output chunks per tile (12 kGroups / 16)
@@ -294,19 +288,12 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
     build_dec_lut(lut);
     __syncthreads();
 
-    uint64_t t0, t1, step = 1;
-    if (ORDERED) {
-        t0 = blockIdx.x;
-        t1 = ntiles;
-        step = gridDim.x;
-    } else {
-        tile_range(ntiles, t0, t1);
-    }
+    uint64_t t0, t1;
+    tile_range(ntiles, t0, t1);
     if (t0 >= t1) return;
     uint32_t j = find_job(jobs, njobs, t0);
-    for (uint64_t t = t0; t < t1; t += step) {
-        if (ORDERED) j = find_job(jobs, njobs, t);
-        else while (jobs[j + 1].tile_start <= t) ++j;
+    for (uint64_t t = t0; t < t1; ++t) {
+        while (jobs[j + 1].tile_start <= t) ++j;
         const uint8_t* __restrict__ src = reinterpret_cast<const uint8_t*>(in) + jobs[j].src_off;
         uint8_t* __restrict__ dst = out + jobs[j].dst_off;
         const DecGeom G = dec_geom(jobs[j].len, reinterpret_cast<uintptr_t>(dst));
@@ -364,11 +351,7 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
         }
         if (threadIdx.x < 64 && t + 1 == jobs[j + 1].tile_start)  // wave 0 of the message's last tile
             dec_tail(lut, jobs[j], G, src, dst, status, out_len);
-        __syncthreads();  // stream[] is rewritten by the next tile; every wave's stores of this tile are done
-        if (ORDERED && threadIdx.x == 0) {
-            __threadfence();  // agent scope: the tile's bytes reach every XCD before the count does
-            __hip_atomic_fetch_add(done + jobs[j].aux, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        __syncthreads();  // stream[] is rewritten by the next tile
     }
 }
 
@@ -383,14 +366,10 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 }
 
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                             int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t* done, uint32_t wgs_per_cu) {
+                             int32_t* status, uint64_t* out_len, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
-    if (done)
-        hipLaunchKernelGGL(b64_decode_kernel<true>, dim3(stream_grid(ntiles, wgs_per_cu)), dim3(kStreamBlock), 0, s, in,
-                           jobs, njobs, ntiles, out, status, out_len, done);
-    else
-        hipLaunchKernelGGL(b64_decode_kernel<false>, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, in, jobs,
-                           njobs, ntiles, out, status, out_len, nullptr);
+    hipLaunchKernelGGL(b64_decode_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, in, jobs, njobs, ntiles,
+                       out, status, out_len);
     return hipGetLastError();
 }
 

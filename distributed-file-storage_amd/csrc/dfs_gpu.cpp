@@ -52,7 +52,7 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_QUEUE, B_WAIT, B_COUNT };
+enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_QUEUE, B_COUNT };
 
 }  // namespace
 
@@ -1119,7 +1119,6 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
             j.dst_off = file_off[f] + off[i];
             j.expect = len[i] + 1;
             j.id = static_cast<uint32_t>(k);
-            j.aux = f;  // decode-progress counter of the file (overlapped path)
             jobs.push_back(j);
             items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
             sha.push_back(msg(file_off[f] + off[i], len[i], k));
@@ -1128,72 +1127,31 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     }
     const uint32_t njobs = static_cast<uint32_t>(jobs.size());
     const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
-    // Large batches overlap the two passes: the decode runs in file order on
-    // this stream, the persistent SHA kernel beside it on the aux stream, and
-    // every SHA lane first waits until its file's tiles are decoded (the
-    // kernel's kShaWait counters).  Small batches (latency kernel) run the
-    // passes back to back.
-    const bool overlap = sha.size() > dfs::kChainMaxLanes;
-    if (overlap) {
-        std::vector<uint32_t> tiles(nfiles, 0);
-        for (uint32_t q = 0; q < njobs; ++q) tiles[jobs[q].aux] += static_cast<uint32_t>(jobs[q + 1].tile_start - jobs[q].tile_start);
-        for (ShaDesc& d : sha) {
-            const uint32_t f = d.out >= nf ? static_cast<uint32_t>(d.out - nf) : static_cast<uint32_t>(d.out / nfrag);
-            d.flags |= dfs::kShaWait;
-            d.b64 = (static_cast<uint64_t>(f) << 32) | tiles[f];
-        }
-    }
-    const uint32_t prio = sort_lanes(sha);  // one message per lane
+    const uint32_t prio = sort_lanes(sha);  // one message per lane, persistent sha256_lanes
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * nf));
     HIPC(c->buf[B_DIG0].ensure(32ull * (nf + nfiles)));
     HIPC(hipMemsetAsync(c->buf[B_STATUS].p, 0, 4ull * nf, s));
-    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
-    uint32_t* d_wait = nullptr;
-    hipStream_t sh = s;  // SHA stream
-    if (overlap) {
-        HIPC(c->buf[B_WAIT].ensure(4ull * nfiles));
-        d_wait = c->buf[B_WAIT].as<uint32_t>();
-        HIPC(hipMemsetAsync(d_wait, 0, 4ull * nfiles, s));
-        if (!c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-        sh = c->aux;
-    }
     tm.begin(DFS_T_TOTAL, s);
-    if (overlap) {  // fork
-        HIPC(hipEventRecord(c->fork, s));
-        HIPC(hipStreamWaitEvent(sh, c->fork, 0));
-    }
     tm.begin(DFS_T_B64DEC, s);
-    // beside the SHA kernel (3 x 116-VGPR waves per SIMD) one 4-wave decode
-    // workgroup per CU fits
     HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out,
-                                c->buf[B_STATUS].as<int32_t>(), nullptr, s, d_wait, overlap ? 1u : 8u));
+                                c->buf[B_STATUS].as<int32_t>(), nullptr, s));
     tm.end(DFS_T_B64DEC, s);
-    tm.begin(DFS_T_SHA, sh);
+    tm.begin(DFS_T_SHA, s);
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
                             static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(),
-                            overlap ? c->sha_wps_beside : c->sha_wps, sh, nullptr, nullptr, d_wait));
-    tm.end(DFS_T_SHA, sh);
-    if (overlap) {  // join
-        HIPC(hipEventRecord(c->join, sh));
-        HIPC(hipStreamWaitEvent(s, c->join, 0));
-    }
+                            c->sha_wps, s));
+    tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
-    uint32_t wait_timeout = 0;
-    if (overlap)
-        HIPC(hipMemcpyAsync(&wait_timeout, c->buf[B_QUEUE].as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, s));
     std::vector<int32_t> st(nf);
     std::vector<uint8_t> dig(32ull * (nf + nfiles));
     HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * nf, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
     if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    if (wait_timeout) {  // a SHA lane gave up waiting for the decode (never expected)
-        std::snprintf(g_last_hip, sizeof g_last_hip, "dfs_download_batch: SHA-256 lanes timed out waiting for the decode");
-        return DFS_E_HIP;
-    }
     std::vector<uint8_t> expf, expd;
     if (dev && exp_frag && is_device_ptr(exp_frag)) {  // expected digests may live on the device in device mode
         expf.resize(32ull * nf);

@@ -30,11 +30,6 @@ constexpr uint32_t kShaPartial = 2u;
 // kShaB64: also write the RFC 4648 Base64 of the message at b64out + b64
 // (fused upload encode; whole messages only, never with Resume/Partial).
 constexpr uint32_t kShaB64 = 4u;
-// kShaWait: before hashing, wait until wait[b64 >> 32] >= (uint32_t)b64 (the
-// download's decode-progress counters, set by b64_decode_kernel<ORDERED>);
-// a wait longer than kShaWaitTicks sets queue[2] and the lane skips.
-constexpr uint32_t kShaWait = 8u;
-constexpr uint64_t kShaWaitTicks = 1000000000ull;  // 10 s of s_memrealtime (100 MHz)
 
 // One byte-stream job for the tiled HBM-bound kernels (Base64 encode/decode,
 // gather, synth).  Jobs are sorted by tile_start; a sentinel job with
@@ -123,8 +118,7 @@ struct BodyParse {
 // the 1024 SIMDs (fewer for small batches).
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
-                         int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr,
-                         const uint32_t* wait = nullptr);
+                         int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr);
 // Tiles hold kEncPer*256 12-byte groups (the job table's tile_start must be
 // built with that tile size); prio = s_setprio of the encode waves.
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
@@ -133,11 +127,8 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 // status[id] |= 1 on an IllegalArgumentException case; out_len[id] = bytes.
 // If job.expect != 0 it is the expected decoded length + 1 (download path):
 // a different length sets status bit 2.  Tiles hold kDecGpl*256 4-unit groups.
-// done != NULL: tiles in grid-stride order and done[job.aux] += 1 per tile
-// (decode-progress counters for kShaWait lanes), wgs_per_cu workgroups per CU.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s,
-                             uint32_t* done = nullptr, uint32_t wgs_per_cu = 8);
+                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s);
 // Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
 hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
                                    hipStream_t s);

@@ -365,30 +365,12 @@ __device__ __forceinline__ uint32_t simd_key() {
 // token counters; all zeroed by the launcher before each launch.
 // ENC = the fused-Base64 instantiation (launched when the caller passes a
 // Base64 output; lanes flagged kShaB64 also write their message's Base64).
-// Wait (kShaWait) until the decode kernel running beside this one finished
-// the lane's file: wait[idx] >= need, read with agent-scope acquire so the
-// decoded bytes written before the count are seen.  Bounded: after
-// kShaWaitTicks the lane gives up, flags queue[2] and is skipped (the host
-// reports the call as failed), so the persistent grid always drains.
-__device__ __forceinline__ bool wait_decoded(const uint32_t* __restrict__ wait, uint64_t w, uint32_t* queue) {
-    const uint32_t idx = static_cast<uint32_t>(w >> 32), need = static_cast<uint32_t>(w);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(wait + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
-        __builtin_amdgcn_s_sleep(8);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kShaWaitTicks) {
-            atomicOr(queue + 2, 1u);
-            return false;
-        }
-    }
-    return true;
-}
-
 template <bool ENC>
 __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
                                             uint32_t n, uint32_t split, uint32_t n_long, uint32_t cap,
                                             uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
                                             uint32_t* __restrict__ queue, uint32_t* __restrict__ state,
-                                            char* __restrict__ b64, const uint32_t* __restrict__ wait) {
+                                            char* __restrict__ b64) {
     const uint32_t nitems = (n + 63u) >> 6;
     const uint32_t n_short = nitems - n_long;
     const uint32_t lane = threadIdx.x & 63u;
@@ -432,9 +414,7 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
         const uint32_t kmax =
             ENC ? __builtin_amdgcn_readfirstlane(wave_max(gid < n ? static_cast<uint32_t>(descs[gid].len >> 6) : 0u))
                 : 0u;
-        bool go = gid < n;
-        if (!ENC && wait && go && (descs[gid].flags & kShaWait)) go = wait_decoded(wait, descs[gid].b64, queue);
-        if (go) {
+        if (gid < n) {
             const Msg m = msg_setup(base, descs[gid]);
             uint32_t st[8];
             if (m.flags & kShaResume) {
@@ -675,17 +655,16 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
 #define DFS_SHA_ARGS                                                                                     \
     const uint8_t *__restrict__ base, const ShaDesc *__restrict__ descs, uint32_t n, uint32_t split,       \
         uint32_t n_long, uint32_t cap, uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,             \
-        uint32_t *__restrict__ queue, uint32_t *__restrict__ state, char *__restrict__ b64,                 \
-        const uint32_t *__restrict__ wait
+        uint32_t *__restrict__ queue, uint32_t *__restrict__ state, char *__restrict__ b64
 // Plain (hash only).  The pair-fetch block loop measured 76.6 ms alone on
 // config 2 (78.8 ms with two register buffers, 79.4 ms with one compression
 // per iteration); beside Base64 91.3 / 93.1 / 93.9 ms.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes(DFS_SHA_ARGS) {
-    sha256_body<false>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64, wait);
+    sha256_body<false>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64);
 }
 // Fused: fragment lanes flagged kShaB64 also write their Base64.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
-    sha256_body<true>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64, nullptr);
+    sha256_body<true>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64);
 }
 #undef DFS_SHA_ARGS
 
@@ -693,9 +672,9 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
-                         hipStream_t s, uint32_t* state, char* b64, const uint32_t* wait) {
+                         hipStream_t s, uint32_t* state, char* b64) {
     if (n == 0) return hipSuccess;
-    if (!b64 && !wait && n <= kChainMaxLanes) {  // latency-bound launch: owner + helper waves
+    if (!b64 && n <= kChainMaxLanes) {  // latency-bound launch: owner + helper waves
         hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, split, out0,
                            out1, state);
         return hipGetLastError();
@@ -710,10 +689,10 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     if (b64) {
         hipLaunchKernelGGL(sha256_lanes_b64, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
-                           out0, out1, queue, state, b64, nullptr);
+                           out0, out1, queue, state, b64);
     } else {
         hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
-                           out1, queue, state, nullptr, wait);
+                           out1, queue, state, nullptr);
     }
     return hipGetLastError();
 }

@@ -635,9 +635,8 @@ def test_sha256_both_kernels_large_and_small_launches(engine):
 
 
 def test_download_overlapped_large_batch(engine):
-    """Batches above dfs::kChainMaxLanes SHA lanes overlap the Base64 decode
-    (file order, progress counters) with the persistent SHA kernel, whose
-    lanes wait for their file's decode.  6,000 files (36,000 lanes): every
+    """A download above dfs::kChainMaxLanes SHA lanes (the persistent SHA
+    kernel after the decode).  6,000 files (36,000 lanes): every
     file rebuilt and verified, plus the failure statuses on a few files —
     missing fragment (SN:443-446), invalid Base64 (SN:281), wrong fragment
     digest (SN:250-257), wrong fileId (SN:455-458) — and their neighbours
