@@ -102,6 +102,9 @@ def parse(argv=None):
     ap.add_argument("--placement", choices=("star", "ring"), default="star",
                     help="N>1: placement inside the timed step (the other one is timed beside it)")
     ap.add_argument("--chunks", type=int, default=4, help="N>1: file chunks pipelined through compute + placement")
+    ap.add_argument("--placement-step", action="store_true",
+                    help="run the N>1 step (upload + RCCL placement, degraded read) at N=1 too: a one-rank "
+                         "communicator, every node on this GPU (checks that code path on a one-GPU box)")
     ap.add_argument("--no-download", action="store_true", help="skip the download/verify leg")
     ap.add_argument("--dl-steps", type=int, default=2)
     ap.add_argument("--wire-files", type=int, default=16384, help="files in the storeFragments body leg")
@@ -121,7 +124,7 @@ def parse(argv=None):
 
 
 def resolve_config(args, world: int) -> None:
-    cfg = args.config or (2 if world == 1 else 3)
+    cfg = args.config or (2 if world == 1 and not args.placement_step else 3)
     args.config = cfg
     if cfg == 3:  # BASELINE configs[2]: 1M files x 256 KiB sharded by file over 8 GPUs, N = 8
         F, S, N = 131072, 256 << 10, 8
@@ -700,12 +703,15 @@ def multi_gpu(args, world, rank, local, log):
     # Degraded read (BASELINE configs[4]): the last GPU offline; every other
     # rank fetches its groups back from the live holders (SN:422-446), then
     # Base64-decodes them into place with per-fragment and fileId verify.
-    offline = [world - 1]
+    # (One rank alone: nobody offline, the fetch is local.)
+    offline = [world - 1] if world > 1 else []
     fetch_ms = dl_ms = 0.0
     dl_ok = True
     out = torch.empty(max(sh.chunks[0]["b"] - sh.chunks[0]["a"], 1) * S, dtype=torch.uint8, device=dev)
     back = torch.empty(max(ch["grp"][-1] for ch in sh.chunks), dtype=torch.uint8, device=dev)
     for ch in sh.chunks:
+        nf = ch["b"] - ch["a"]
+        spans_c = ch["plan"].b64_spans([S] * nf)
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
@@ -714,10 +720,9 @@ def multi_gpu(args, world, rank, local, log):
         fetch_ms += (time.perf_counter() - t0) * 1e3
         if rank in offline:
             continue
-        nf = ch["b"] - ch["a"]
         dl_ok &= bool((st == 0).all()) and bool(torch.equal(back[:ch["grp"][-1]], ch["b64"][:ch["grp"][-1]]))
         t0 = time.perf_counter()
-        status = download_device(eng_c, back.data_ptr(), ch["plan"].b64_spans([S] * nf), nf, N,
+        status = download_device(eng_c, back.data_ptr(), spans_c, nf, N,
                                  np.full(nf, S, np.uint64), sh.frd.data_ptr() + 32 * N * ch["a"],
                                  sh.fd.data_ptr() + 32 * ch["a"], out.data_ptr(),
                                  np.arange(nf, dtype=np.uint64) * np.uint64(S))
@@ -742,7 +747,8 @@ def multi_gpu(args, world, rank, local, log):
             "ring_xgmi_gbps_per_gpu": round(sent_t[0].item() / world / t_place["ring"] / 1e9, 2),
             "bytes_sent_per_gpu": {"star": int(sent_t[1].item() / world), "ring": int(sent_t[0].item() / world)},
             "held_bytes_per_gpu": held_bytes, "ring_equals_star": ok,
-            "degraded": {"offline_gpu": world - 1, "fetch_ms": round(fetch_ms, 3), "download_ms": round(dl_ms, 3),
+            "degraded": {"offline_gpu": offline[0] if offline else None, "fetch_ms": round(fetch_ms, 3),
+                         "download_ms": round(dl_ms, 3),
                          "download_gbps": round(F * S / (dl_ms / 1e3) / 1e9, 2) if dl_ms else None,
                          "ok": ok_all},
             "note": "xgmi_gbps = bytes this GPU sends / placement time (RCCL send/recv, dfs_place_ring / "
@@ -849,10 +855,14 @@ def main():
     import torch.distributed as dist
     import dfs_amd
 
-    if world > 1:
+    if world > 1 or args.placement_step:
         import datetime
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=600))
         S, N, F = args.file_size, args.nfrag, args.files
         failures = []

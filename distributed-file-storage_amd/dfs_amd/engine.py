@@ -517,8 +517,11 @@ class UploadPlan:
         order; lengths come from the split, so they are exact with the
         align128 gaps too."""
         off = self.b64_offsets()
-        lens = np.array([4 * ((ln + 2) // 3) for fl in file_lens for _, ln in split_plan(int(fl), self.nfrag)],
-                        dtype=np.uint64)
+        fl = np.asarray(file_lens, dtype=np.uint64).reshape(-1, 1)
+        i = np.arange(self.nfrag, dtype=np.uint64).reshape(1, -1)
+        n = np.uint64(self.nfrag)
+        frag = fl // n + (i < fl % n).astype(np.uint64)  # the split of SN:138-171 (dfs_split_plan)
+        lens = (np.uint64(4) * ((frag + np.uint64(2)) // np.uint64(3))).reshape(-1)
         return np.stack([off[:-1], lens], axis=1).astype(np.uint64)
 
     def run(self, d_files: int, d_file_digest: int, d_frag_digest: int, d_b64: int, flags: int = 0) -> None:
