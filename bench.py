@@ -475,7 +475,7 @@ def batcher_leg(args, log):
             p = subprocess.run([tool, str(C), str(args.client_seconds), kind, str(S), str(N), "500", "3"],
                                capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
-                raise LegError(f"batcher_load {C} {kind}: rc {p.returncode}: {p.stderr[-300:]}")
+                raise LegError(f"batcher_load {C} {kind}: rc {p.returncode}: {p.stderr[-300:]} {p.stdout[-300:]}")
             r = json.loads(p.stdout.strip().splitlines()[-1])
             ok &= r["ok"] and [r["file0_id"], r["file1_id"]] == want
             row[kind] = {k: r[k] for k in ("requests", "gbps", "p50_ms", "p99_ms")}
@@ -1027,8 +1027,6 @@ def main():
         legs.append(("store", lambda: store_leg(args, eng, files, fd, S, N, F, dev, log)))
     if not args.no_cpu_baseline:
         legs.append(("cpu_baseline", lambda: cpu_baseline(args, log)))
-    if not args.no_batcher:
-        legs.append(("batcher", lambda: batcher_leg(args, log)))
     for name, fn in legs:
         try:
             result[name] = fn()
@@ -1037,10 +1035,25 @@ def main():
             traceback.print_exc()
             result[name] = {"error": repr(e)[:300]}
             failures.append(name)
+    # The concurrent-clients leg runs in a child process with its own device
+    # buffers: hand back the upload's 160 GB first.
+    if not args.no_batcher:
+        plan.close()
+        del files, b64, fd, frd, legs
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        try:
+            result["batcher"] = batcher_leg(args, log)
+        except Exception as e:
+            import traceback
+            traceback.print_exc()
+            result["batcher"] = {"error": repr(e)[:600]}
+            failures.append("batcher")
     if failures:
         result["failed_legs"] = failures
     print(json.dumps(result), flush=True)
-    plan.close()
+    if args.no_batcher:
+        plan.close()
     eng.close()
     return 3 if failures else 0
 

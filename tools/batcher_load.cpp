@@ -106,6 +106,7 @@ int main(int argc, char** argv) {
     }
     std::atomic<int> ready{0};
     std::atomic<bool> go{false}, bad{false};
+    std::atomic<int> first_rc{0}, mismatches{0};
     std::vector<std::vector<double>> lat(C);
     Clock::time_point deadline, measure_from;
     std::vector<std::thread> th;
@@ -130,13 +131,16 @@ int main(int argc, char** argv) {
                 }
                 const auto t1 = Clock::now();
                 if (t0 >= measure_from) lat[t].push_back(std::chrono::duration<double>(t1 - t0).count());
-                if (rc != DFS_OK) bad = true;
-                else if (it % 8) {  // every 8th result is compared in full (the handler's own work stays small)
+                if (rc != DFS_OK) {
+                    bad = true;
+                    int z = 0;
+                    first_rc.compare_exchange_strong(z, rc);
+                } else if (it % 8) {  // every 8th result is compared in full (the handler's own work stays small)
                 } else if (up && (std::memcmp(mfd.data(), fd[f].data(), 32) || std::memcmp(mfrd.data(), frd[f].data(), 32 * N) ||
                                 std::memcmp(mb.data(), b64[f].data(), off[f][N])))
-                    bad = true;
+                    bad = true, ++mismatches;
                 else if (!up && std::memcmp(out.data(), file[f].data(), S))
-                    bad = true;
+                    bad = true, ++mismatches;
                 if (t1 >= deadline) break;
             }
         });
@@ -171,5 +175,8 @@ int main(int argc, char** argv) {
                 hex(fd[1].data()).c_str(), (unsigned long long)st.batches, (unsigned long long)st.requests,
                 (unsigned long long)st.max_batch, st.queue_s, st.stage_in_s, st.device_s, st.stage_out_s, st.enqueue_s,
                 st.return_s);
+    if (bad)
+        std::fprintf(stderr, "batcher_load: %d mismatching results, first failing status %d (%s)\n", mismatches.load(),
+                     first_rc.load(), first_rc.load() ? dfs_strerror(first_rc.load()) : "-");
     return bad ? 1 : 0;
 }
