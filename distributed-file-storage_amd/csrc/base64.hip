@@ -279,7 +279,8 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
                                                                   uint32_t njobs, uint64_t ntiles,
                                                                   uint8_t* __restrict__ out,
                                                                   int32_t* __restrict__ status,
-                                                                  uint64_t* __restrict__ out_len) {
+                                                                  uint64_t* __restrict__ out_len, uint32_t prio) {
+    if (prio) __builtin_amdgcn_s_setprio(3);  // beside the SHA kernel (pipelined download)
     constexpr int GPL = kDecGpl;
     constexpr uint32_t kGroups = GPL * kStreamBlock;  // 4-unit groups per tile
     constexpr uint32_t kChunks = 3 * GPL * 64;        // 16-byte output chunks per tile (12 kGroups / 16)
@@ -366,10 +367,10 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 }
 
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                             int32_t* status, uint64_t* out_len, hipStream_t s) {
+                             int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t prio, uint32_t wgs_per_cu) {
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(b64_decode_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, in, jobs, njobs, ntiles,
-                       out, status, out_len);
+    hipLaunchKernelGGL(b64_decode_kernel, dim3(stream_grid(ntiles, wgs_per_cu)), dim3(kStreamBlock), 0, s, in, jobs, njobs, ntiles,
+                       out, status, out_len, prio);
     return hipGetLastError();
 }
 

@@ -67,11 +67,15 @@ struct dfs_ctx {
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
     int sha_wps_beside = 3;      // ... when the Base64 kernel runs beside it (4 x 116 VGPRs leave no room)
     int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels (DFS_UPLOAD_MODE)
+    int download_mode = 0;       // 0 pipelined by fragment (decode || SHA), 1 decode then SHA (DFS_DOWNLOAD_MODE)
     int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
+    uint32_t dec_prio = 1;       // decode waves at s_setprio 3 beside SHA (DFS_DEC_PRIO=0: 0)
+    uint32_t dec_wgs = 1;        // decode workgroups per CU beside SHA (DFS_DEC_WGS)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
     hipEvent_t fork = nullptr, join = nullptr;  // SHA || Base64 on two streams
+    std::vector<hipEvent_t> pass_ev;             // download passes (decode of fragment i done)
     // The scratch buffers (buf[]) are reused by the next call.  An async call
     // leaves them in use on its stream: a call on another stream (after
     // dfs_set_stream) first waits for scratch_ev (recorded after the last
@@ -325,8 +329,11 @@ int dfs_open(dfs_ctx** out, int device) {
     c->device = device;
     if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = c->sha_wps_beside = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_UPLOAD_MODE")) c->upload_mode = std::strcmp(w, "fused") == 0 ? 0 : 1;
+    if (const char* w = std::getenv("DFS_DOWNLOAD_MODE")) c->download_mode = std::strcmp(w, "serial") == 0 ? 1 : 0;
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
+    if (const char* w = std::getenv("DFS_DEC_PRIO")) c->dec_prio = std::atoi(w) ? 1u : 0u;
+    if (const char* w = std::getenv("DFS_DEC_WGS")) c->dec_wgs = static_cast<uint32_t>(std::max(1, std::min(8, std::atoi(w))));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     for (int i = 0; e == hipSuccess && i < 2 * DFS_T_COUNT; ++i) e = hipEventCreate(&c->ev[i]);
@@ -354,6 +361,7 @@ int dfs_close(dfs_ctx* c) {
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : {c->fork, c->join, c->scratch_ev})
         if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : c->pass_ev) (void)hipEventDestroy(ev);
     for (auto& a : c->arena) {
         if (a.ev) (void)hipEventDestroy(a.ev);
         if (a.p) (void)hipHostFree(a.p);
@@ -1104,47 +1112,109 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         d_out = c->buf[B_DATA_OUT].as<uint8_t>();
     }
     // Decode jobs write straight into the file at the split offsets (fused gather).
-    std::vector<StreamJob> jobs;
+    // Large batches run in passes over fragment groups {0}, {1, 2}, {3..6}, ...:
+    // pass p decodes its group of every file on s while the aux stream hashes
+    // pass p - 1's fragments and advances every fileId over them (state in
+    // HBM between launches, kShaResume / kShaPartial), so the SHA starts after
+    // one fragment's decode instead of the whole batch's, and each decode pass
+    // runs beside a SHA launch about as long as itself.  A fileId part ends on
+    // the last 64-byte boundary inside its group, so it reads decoded bytes only.
+    uint64_t nok = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) nok += status[f] == DFS_OK;
+    const bool pipe = c->download_mode == 0 && nfrag > 1 && nok * (nfrag + 1) > dfs::kChainMaxLanes;
+    std::vector<uint32_t> gb{0};  // group p = fragments [gb[p], gb[p + 1])
+    for (uint32_t w = 1; gb.back() < nfrag; w *= 2) gb.push_back(pipe ? std::min(nfrag, gb.back() + w) : nfrag);
+    const uint32_t npass = static_cast<uint32_t>(gb.size() - 1);
+    std::vector<StreamJob> jobs, pjobs;
     std::vector<uint64_t> items;
-    std::vector<ShaDesc> sha;  // fragments (out = k) then files (out = nf + f)
+    std::vector<ShaDesc> sha, psha;  // per pass: fragments (out = k), files (out = nf + f)
+    std::vector<uint64_t> job0(npass + 1, 0), desc0(npass + 1, 0), tiles(npass);
+    std::vector<uint32_t> prio(npass);
     std::vector<uint64_t> off(nfrag), len(nfrag);
-    for (uint32_t f = 0; f < nfiles; ++f) {
-        if (status[f] != DFS_OK) continue;
-        split(file_len[f], nfrag, off.data(), len.data());
-        for (uint32_t i = 0; i < nfrag; ++i) {
-            const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
-            StreamJob j{};
-            j.src_off = msgs[k].off;
-            j.len = msgs[k].len;
-            j.dst_off = file_off[f] + off[i];
-            j.expect = len[i] + 1;
-            j.id = static_cast<uint32_t>(k);
-            jobs.push_back(j);
-            items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
-            sha.push_back(msg(file_off[f] + off[i], len[i], k));
+    for (uint32_t p = 0; p < npass; ++p) {
+        pjobs.clear();
+        items.clear();
+        psha.clear();
+        for (uint32_t f = 0; f < nfiles; ++f) {
+            if (status[f] != DFS_OK) continue;
+            split(file_len[f], nfrag, off.data(), len.data());
+            for (uint32_t i = gb[p]; i < gb[p + 1]; ++i) {
+                const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+                StreamJob j{};
+                j.src_off = msgs[k].off;
+                j.len = msgs[k].len;
+                j.dst_off = file_off[f] + off[i];
+                j.expect = len[i] + 1;
+                j.id = static_cast<uint32_t>(k);
+                pjobs.push_back(j);
+                items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
+                psha.push_back(msg(file_off[f] + off[i], len[i], k));
+            }
+            const bool first = p == 0, last = p + 1 == npass;
+            const uint64_t a = first ? 0 : off[gb[p]] & ~63ull, e = last ? file_len[f] : off[gb[p + 1]] & ~63ull;
+            ShaDesc d = msg(file_off[f] + a, e - a, nf + f);
+            d.total = file_len[f];
+            d.flags = (first ? 0u : dfs::kShaResume) | (last ? 0u : dfs::kShaPartial);
+            psha.push_back(d);
         }
-        sha.push_back(msg(file_off[f], file_len[f], nf + f));
+        tiles[p] = finish_jobs(pjobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
+        prio[p] = sort_lanes(psha);  // one message per lane, longest first
+        // Long items (balanced per SIMD, sha256_body): the fileId parts, which
+        // are |group| fragments long; in a one-fragment pass every lane is
+        // about one fragment long, so every item counts as long.
+        if (pipe) prio[p] = static_cast<uint32_t>(gb[p + 1] - gb[p] == 1 ? psha.size() : nok);
+        jobs.insert(jobs.end(), pjobs.begin(), pjobs.end());
+        sha.insert(sha.end(), psha.begin(), psha.end());
+        job0[p + 1] = jobs.size();
+        desc0[p + 1] = sha.size();
     }
-    const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
-    const uint32_t prio = sort_lanes(sha);  // one message per lane, persistent sha256_lanes
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * nf));
     HIPC(c->buf[B_DIG0].ensure(32ull * (nf + nfiles)));
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(hipMemsetAsync(c->buf[B_STATUS].p, 0, 4ull * nf, s));
     uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
+    const StreamJob* d_jobs = c->buf[B_JOBS].as<StreamJob>();
+    const ShaDesc* d_desc = c->buf[B_DESC].as<ShaDesc>();
+    int32_t* d_st = c->buf[B_STATUS].as<int32_t>();
+    uint32_t* d_queue = c->buf[B_QUEUE].as<uint32_t>();
+    const uint32_t nout = static_cast<uint32_t>(nf + nfiles);
     tm.begin(DFS_T_TOTAL, s);
-    tm.begin(DFS_T_B64DEC, s);
-    HIPC(dfs::launch_b64_decode(d_in, c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out,
-                                c->buf[B_STATUS].as<int32_t>(), nullptr, s));
-    tm.end(DFS_T_B64DEC, s);
-    tm.begin(DFS_T_SHA, s);
-    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
-    HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()),
-                            static_cast<uint32_t>(nf + nfiles), prio, d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(),
-                            c->sha_wps, s));
-    tm.end(DFS_T_SHA, s);
+    if (!pipe) {
+        tm.begin(DFS_T_B64DEC, s);
+        HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(jobs.size()), tiles[0], d_out, d_st, nullptr, s));
+        tm.end(DFS_T_B64DEC, s);
+        tm.begin(DFS_T_SHA, s);
+        HIPC(dfs::launch_sha256(d_out, d_desc, static_cast<uint32_t>(sha.size()), nout, prio[0], d_dig, d_dig, d_queue,
+                                c->sha_wps, s));
+        tm.end(DFS_T_SHA, s);
+    } else {
+        HIPC(c->buf[B_DIG1].ensure(32ull * nout));  // running fileId states
+        uint32_t* d_state = c->buf[B_DIG1].as<uint32_t>();
+        if (!c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        while (c->pass_ev.size() < npass) {
+            hipEvent_t ev = nullptr;
+            HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            c->pass_ev.push_back(ev);
+        }
+        tm.begin(DFS_T_B64DEC, s);
+        for (uint32_t p = 0; p < npass; ++p) {
+            HIPC(dfs::launch_b64_decode(d_in, d_jobs + job0[p], static_cast<uint32_t>(job0[p + 1] - job0[p]), tiles[p],
+                                        d_out, d_st, nullptr, s, c->dec_prio, p ? c->dec_wgs : 8u));
+            HIPC(hipEventRecord(c->pass_ev[p], s));
+        }
+        tm.end(DFS_T_B64DEC, s);
+        for (uint32_t p = 0; p < npass; ++p) {
+            HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[p], 0));
+            if (p == 0) tm.begin(DFS_T_SHA, c->aux);
+            HIPC(dfs::launch_sha256(d_out, d_desc + desc0[p], static_cast<uint32_t>(desc0[p + 1] - desc0[p]), nout,
+                                    prio[p], d_dig, d_dig, d_queue, c->sha_wps_beside, c->aux, d_state));
+        }
+        tm.end(DFS_T_SHA, c->aux);
+        HIPC(hipEventRecord(c->join, c->aux));
+        HIPC(hipStreamWaitEvent(s, c->join, 0));
+    }
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(nf);
     std::vector<uint8_t> dig(32ull * (nf + nfiles));

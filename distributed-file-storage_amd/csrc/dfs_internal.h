@@ -127,8 +127,11 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 // status[id] |= 1 on an IllegalArgumentException case; out_len[id] = bytes.
 // If job.expect != 0 it is the expected decoded length + 1 (download path):
 // a different length sets status bit 2.  Tiles hold kDecGpl*256 4-unit groups.
+// prio != 0: the waves run at s_setprio 3 (beside the SHA kernel); the grid
+// holds at most wgs_per_cu persistent workgroups per CU.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
-                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s);
+                             uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t prio = 0,
+                             uint32_t wgs_per_cu = 8);
 // Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
 hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
                                    hipStream_t s);

@@ -365,6 +365,8 @@ __device__ __forceinline__ uint32_t simd_key() {
 // token counters; all zeroed by the launcher before each launch.
 // ENC = the fused-Base64 instantiation (launched when the caller passes a
 // Base64 output; lanes flagged kShaB64 also write their message's Base64).
+constexpr uint32_t kStealSpins = 16;  // x s_sleep 127 (8,128 clocks each)
+
 template <bool ENC>
 __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
                                             uint32_t n, uint32_t split, uint32_t n_long, uint32_t cap,
@@ -395,9 +397,20 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                 const uint32_t it = atomicAdd(queue + 1, 1u);
                 if (it < n_short) {
                     item = n_long + it;
-                } else if (n_long) {  // long items a starved SIMD left behind
-                    const uint32_t it2 = atomicAdd(queue, 1u);
-                    if (it2 < n_long) item = it2;
+                } else if (n_long) {
+                    // Long items a starved SIMD left behind (one that got fewer
+                    // than `cap` waves).  Taken only after the SIMDs that have
+                    // waves claimed theirs (~50 us), so a launch whose items
+                    // are all long keeps exactly `cap` per SIMD.
+                    for (uint32_t spin = 0;; ++spin) {
+                        if (__hip_atomic_load(queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n_long) break;
+                        if (spin == kStealSpins) {
+                            const uint32_t it2 = atomicAdd(queue, 1u);
+                            if (it2 < n_long) item = it2;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(127);
+                    }
                 }
             }
         }
@@ -685,7 +698,7 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     const uint32_t cap = (n_long + 1023u) / 1024u;
     const uint64_t items = (n + 63u) / 64u;
     uint64_t waves = 1024ull * static_cast<uint64_t>(waves_per_simd < 1 ? 1 : waves_per_simd);
-    if (waves > items) waves = items;
+    if (waves > items && !n_long) waves = items;  // with long items the spare waves keep SIMDs balanced
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     if (b64) {
         hipLaunchKernelGGL(sha256_lanes_b64, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,

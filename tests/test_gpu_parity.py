@@ -634,13 +634,21 @@ def test_sha256_both_kernels_large_and_small_launches(engine):
     assert all(small[i].tobytes() == want[i] for i in range(5000))
 
 
-def test_download_overlapped_large_batch(engine):
-    """A download above dfs::kChainMaxLanes SHA lanes (the persistent SHA
-    kernel after the decode).  6,000 files (36,000 lanes): every
-    file rebuilt and verified, plus the failure statuses on a few files —
-    missing fragment (SN:443-446), invalid Base64 (SN:281), wrong fragment
-    digest (SN:250-257), wrong fileId (SN:455-458) — and their neighbours
-    unaffected."""
+@pytest.mark.parametrize("mode", ["pipelined", "serial"])
+def test_download_overlapped_large_batch(engine, mode, monkeypatch):
+    """A download above dfs::kChainMaxLanes SHA lanes.  6,000 files (36,000
+    lanes): every file rebuilt and verified, plus the failure statuses on a
+    few files — missing fragment (SN:443-446), invalid Base64 (SN:281), wrong
+    fragment digest (SN:250-257), wrong fileId (SN:455-458), a Base64 char
+    changed to another alphabet char (decodes, digest differs) — and their
+    neighbours unaffected.  Default: pipelined by fragment (pass i decodes
+    fragment i of every file while the fileIds advance over fragment i - 1,
+    their states in HBM between launches); DFS_DOWNLOAD_MODE=serial: the whole
+    decode, then one SHA launch.  One unpadded fragment (valid for the JDK
+    decoder) shifts every later Base64 offset off dword alignment."""
+    if mode == "serial":
+        monkeypatch.setenv("DFS_DOWNLOAD_MODE", "serial")
+        engine = dfs_amd.FragmentEngine(0)
     import base64
     rng = np.random.default_rng(31)
     nfiles, nfrag = 6000, 5
@@ -660,10 +668,44 @@ def test_download_overlapped_large_batch(engine):
     want[2000] = dfs_amd.DFS_E_DECODE
     frag_h[3000] = list(frag_h[3000]); frag_h[3000][4] = "0" * 64
     want[3000] = dfs_amd.DFS_E_FRAG_MISMATCH
+    t = bytearray(texts[4000][3]); t[len(t) // 2] = ord("A") if t[len(t) // 2] != ord("A") else ord("B")
+    texts[4000][3] = bytes(t)
+    want[4000] = dfs_amd.DFS_E_FRAG_MISMATCH
     file_h[5999] = "f" * 64
     want[5999] = dfs_amd.DFS_E_CORRUPT
-    res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+    f = next(f for f in range(7, nfiles) if texts[f][0].endswith(b"="))
+    texts[f][0] = texts[f][0].rstrip(b"=")
+    try:
+        res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+    finally:
+        if mode == "serial":
+            engine.close()
     for f, (st, body) in enumerate(res):
         assert st == want[f], (f, st, want[f])
         if want[f] == 0:
             assert body == files[f], f
+
+
+@pytest.mark.gpu
+def test_download_pipelined_many_fragments_small_files(engine):
+    """The pipelined download with nfrag = 12 and small files: fileId parts of
+    0 bytes in most passes (files under 64 B per fragment), parts ending on
+    every 64-byte boundary case, empty files and fragments; 3,000 files x 13
+    lanes = 39,000 (above dfs::kChainMaxLanes, so the pipelined path)."""
+    import base64
+    rng = np.random.default_rng(77)
+    nfiles, nfrag = 3000, 12
+    sizes = rng.integers(0, 4000, nfiles)
+    edge = [0, 1, 11, 12, 13, 63, 64, 65, 767, 768, 769, 64 * 12, 64 * 12 + 1, 64 * 13 - 1]
+    sizes[:len(edge)] = edge
+    files = [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in sizes]
+    texts, frag_h, file_h = [], [], []
+    for d in files:
+        parts = [d[o:o + n] for o, n in O.c_split(len(d), nfrag)]
+        texts.append([base64.b64encode(p) for p in parts])
+        frag_h.append([hashlib.sha256(p).hexdigest() for p in parts])
+        file_h.append(hashlib.sha256(d).hexdigest())
+    res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+    for f, (st, body) in enumerate(res):
+        assert st == 0, (f, st)
+        assert body == files[f], f
