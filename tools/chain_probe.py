@@ -1,6 +1,8 @@
 """Latency-bound SHA launches: time dfs_sha256_batch over n equal messages
-(device memory) for a sweep of n, under whatever DFS_CHAIN_MAX the process
-has (the chain kernel below it, the persistent kernel above)."""
+(device memory) for a sweep of n.  The library picks the owner/helper chain
+kernel up to dfs::kChainMaxLanes lanes and the persistent kernel above;
+profiles/r02_chain_vs_persistent.txt was measured with a temporary build
+whose threshold came from a DFS_CHAIN_MAX variable (not in the library)."""
 import os
 import sys
 import time
