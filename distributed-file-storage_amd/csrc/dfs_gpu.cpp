@@ -112,6 +112,7 @@ struct dfs_upload_plan {
     uint32_t* d_queue = nullptr;  // SHA work-queue word
     uint32_t nfiles = 0, nfrag = 0;
     uint32_t n_all = 0, n_frag_only = 0;  // SHA lanes with / without fileIds
+    bool twins = false;                   // d_all holds twins behind its n_all lanes (kShaTwin)
     uint32_t prio_all = 0, prio_frag = 0;
     ShaDesc* d_all = nullptr;
     ShaDesc* d_frag = nullptr;
@@ -186,6 +187,41 @@ uint32_t sort_lanes(std::vector<ShaDesc>& d) {
     uint32_t n = 0;
     while (n < d.size() && d[n].len >= 2 * med + 64) ++n;
     return (n + 63) & ~63u;
+}
+
+// Twins (kShaTwin, sha256.hip): a fragment that starts on the 64-byte block
+// grid of its file's fileId lane (or fileId part), is at least one block long
+// and is a whole message rides in that lane: its blocks are loaded and their
+// message schedule expanded once for both digests.  That is fragment 0 of
+// every file (offset 0, SN:153) and, when the fragment size is a multiple of
+// 64 (256 KiB files, N = 8: BASELINE configs[2]), every fragment.  Appends
+// `primary` (with its twin list) and the fragments that are not twins to
+// `lanes`, the twins to `tw` (launched as descs[n_lanes + ...]).  Twins need
+// the persistent kernel: callers enable them only for launches of more than
+// dfs::kChainMaxLanes lanes that run without the fused Base64.
+void add_lane_with_twins(std::vector<ShaDesc>& lanes, std::vector<ShaDesc>& tw, ShaDesc primary,
+                         const ShaDesc* frags, uint32_t nfr, bool enable) {
+    const uint64_t first = tw.size();
+    uint64_t cnt = 0, next = 0;  // first block of the primary a twin may start at
+    const uint64_t pfull = primary.len >> 6;
+    for (uint32_t i = 0; i < nfr; ++i) {
+        const ShaDesc& f = frags[i];
+        const uint64_t rel = f.off - primary.off;
+        const bool ok = enable && f.flags == 0 && f.off >= primary.off && (rel & 63u) == 0 && f.len >= 64 &&
+                        (rel >> 6) >= next && (rel >> 6) + (f.len >> 6) <= pfull;
+        if (ok) {
+            tw.push_back(f);
+            ++cnt;
+            next = (rel >> 6) + (f.len >> 6);
+        } else {
+            lanes.push_back(f);
+        }
+    }
+    if (cnt) {
+        primary.flags |= dfs::kShaTwin;
+        primary.b64 = (cnt << 32) | first;
+    }
+    lanes.push_back(primary);
 }
 
 // Fill tile_start prefix for `items` work items per job; append sentinel.
@@ -715,22 +751,37 @@ namespace {
 // The host half of an upload plan: SHA lanes (fileIds + fragments, and the
 // fragments alone), encode jobs, Base64 layout.
 struct HostPlan {
-    std::vector<ShaDesc> all, frag;
+    std::vector<ShaDesc> all, frag;  // all = n_all lanes (fileIds + fragments) then their twins
     std::vector<StreamJob> enc;
     std::vector<uint64_t> b64_off;
-    uint32_t prio_all = 0, prio_frag = 0;
+    uint32_t prio_all = 0, prio_frag = 0, n_all = 0;
     uint64_t enc_tiles = 0, total = 0;
+    bool twins = false;
 };
 
-int build_host_plan(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint32_t flags, HostPlan& h) {
+// The fileId + fragment lanes of one upload, fragments that can ride in
+// their fileId lane as twins when `twins` (and the launch stays large).
+void build_all_lanes(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, const std::vector<ShaDesc>& frag,
+                     bool twins, HostPlan& h) {
+    std::vector<ShaDesc> tw;
+    h.all.clear();
+    h.all.reserve(nfiles + frag.size());
+    for (uint32_t f = 0; f < nfiles; ++f)  // fileId, SN:127; fragments, SN:159
+        add_lane_with_twins(h.all, tw, msg(files[f].off, files[f].len, f), frag.data() + static_cast<uint64_t>(f) * nfrag,
+                            nfrag, twins);
+    h.twins = !tw.empty();
+    h.n_all = static_cast<uint32_t>(h.all.size());
+    h.all.insert(h.all.end(), tw.begin(), tw.end());
+}
+
+int build_host_plan(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint32_t flags, HostPlan& h,
+                    bool twins = true) {
     const bool frag_major = flags & DFS_LAYOUT_FRAG_MAJOR;
     const uint64_t align = (flags & DFS_LAYOUT_ALIGN128) ? 128 : 1;
     const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
     if (nfiles + nf > 0xffffffffull) return DFS_E_ARG;
-    h.all.clear();
     h.frag.clear();
     h.enc.clear();
-    h.all.reserve(nfiles + nf);
     h.frag.reserve(nf);
     std::vector<uint64_t> items;
     h.enc.reserve(nf + 1);
@@ -739,15 +790,14 @@ int build_host_plan(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint
     std::vector<uint64_t> off(nfrag), len(nfrag);
     for (uint32_t f = 0; f < nfiles; ++f) {
         if (files[f].len >= kMaxMsg) return DFS_E_ARG;
-        h.all.push_back(msg(files[f].off, files[f].len, f));  // fileId, SN:127
-        split(files[f].len, nfrag, off.data(), len.data());   // SN:138-157
+        split(files[f].len, nfrag, off.data(), len.data());  // SN:138-157
         for (uint32_t i = 0; i < nfrag; ++i) {
             const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
-            const ShaDesc d = msg(files[f].off + off[i], len[i], nfiles + k);  // SN:159
-            h.all.push_back(d);
-            h.frag.push_back(d);
+            h.frag.push_back(msg(files[f].off + off[i], len[i], nfiles + k));  // SN:159
         }
     }
+    build_all_lanes(files, nfiles, nfrag, h.frag, twins, h);
+    if (h.twins && h.n_all <= dfs::kChainMaxLanes) build_all_lanes(files, nfiles, nfrag, h.frag, false, h);
     // Base64 layout: [file][fragment] (default) or [fragment][file].
     uint64_t total = 0;
     auto place = [&](uint32_t f, uint32_t i) {
@@ -776,14 +826,22 @@ int build_host_plan(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint
     h.b64_off[nf] = total;
     h.total = total;
     // Fragment lanes carry their Base64 offset: the fused upload encodes in
-    // the SHA pass (kShaB64 is ignored when the kernel gets no output).
-    for (std::vector<ShaDesc>* v : {&h.all, &h.frag})
-        for (ShaDesc& d : *v)
-            if (d.out >= nfiles) {
-                d.b64 = h.b64_off[d.out - nfiles];
-                d.flags |= dfs::kShaB64;
-            }
-    h.prio_all = sort_lanes(h.all);
+    // the SHA pass (kShaB64 is ignored when the kernel gets no output).  A
+    // plan with twins never runs fused (run_plan_locked).
+    for (ShaDesc& d : h.frag) {
+        d.b64 = h.b64_off[d.out - nfiles];
+        d.flags |= dfs::kShaB64;
+    }
+    for (uint32_t i = 0; i < h.n_all; ++i) {
+        ShaDesc& d = h.all[i];
+        if (d.out >= nfiles) {
+            d.b64 = h.b64_off[d.out - nfiles];
+            d.flags |= dfs::kShaB64;
+        }
+    }
+    std::vector<ShaDesc> lanes(h.all.begin(), h.all.begin() + h.n_all);
+    h.prio_all = sort_lanes(lanes);  // twins stay behind the lanes, unsorted
+    std::copy(lanes.begin(), lanes.end(), h.all.begin());
     h.prio_frag = sort_lanes(h.frag);
     h.enc_tiles = finish_jobs(h.enc, items, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
     return DFS_OK;
@@ -795,7 +853,8 @@ void fill_plan_header(dfs_upload_plan* p, const HostPlan& h, int device, uint32_
     p->nfrag = nfrag;
     p->prio_all = h.prio_all;
     p->prio_frag = h.prio_frag;
-    p->n_all = static_cast<uint32_t>(h.all.size());
+    p->n_all = h.n_all;
+    p->twins = h.twins;
     p->n_frag_only = static_cast<uint32_t>(h.frag.size());
     p->n_enc = static_cast<uint32_t>(h.enc.size() - 1);  // minus the sentinel
     p->enc_tiles = h.enc_tiles;
@@ -828,7 +887,7 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     if (flags & ~(DFS_LAYOUT_FRAG_MAJOR | DFS_LAYOUT_ALIGN128)) return DFS_E_ARG;
     *out = nullptr;
     HostPlan h;
-    if (int rc = build_host_plan(files, nfiles, nfrag, flags, h)) return rc;
+    if (int rc = build_host_plan(files, nfiles, nfrag, flags, h, c->upload_mode != 0)) return rc;
     std::lock_guard<std::mutex> lk(c->mu);
     if (int rc = enter(c)) return rc;
     auto* p = new (std::nothrow) dfs_upload_plan;
@@ -877,7 +936,7 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     const bool do_fileid = !(flags & DFS_NO_FILEID);
     const bool do_b64 = !(flags & DFS_NO_B64) && p->n_enc;
     const bool serial = flags & DFS_SERIAL;
-    const bool fused = do_b64 && c->upload_mode == 0 && !serial;
+    const bool fused = do_b64 && c->upload_mode == 0 && !serial && !p->twins;  // twins: plain kernel only
     if (!d_frd || (do_fileid && !d_fd) || (do_b64 && !d_b64)) return DFS_E_ARG;
     if (do_b64 && (reinterpret_cast<uintptr_t>(d_b64) & 3u)) return DFS_E_ARG;
     hipStream_t s = c->stream();
@@ -942,7 +1001,8 @@ int dfs_upload_batch(dfs_ctx* c, const uint8_t* files, const dfs_span* spans, ui
     if (!c || !nfrag || (nfiles && (!spans || !frd))) return DFS_E_ARG;
     if (!(flags & DFS_NO_FILEID) && nfiles && !fd) return DFS_E_ARG;
     HostPlan h;
-    if (int rc = build_host_plan(spans, nfiles, nfrag, flags & DFS_LAYOUT_FRAG_MAJOR, h)) return rc;
+    if (int rc = build_host_plan(spans, nfiles, nfrag, flags & DFS_LAYOUT_FRAG_MAJOR, h, c->upload_mode != 0))
+        return rc;
     const bool do_b64 = !(flags & DFS_NO_B64);
     if (b64_off) std::memcpy(b64_off, h.b64_off.data(), h.b64_off.size() * sizeof(uint64_t));
     if (do_b64 && (h.total > b64_cap || (h.total && !b64))) return DFS_E_ARG;
@@ -1127,14 +1187,33 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     const uint32_t npass = static_cast<uint32_t>(gb.size() - 1);
     std::vector<StreamJob> jobs, pjobs;
     std::vector<uint64_t> items;
-    std::vector<ShaDesc> sha, psha;  // per pass: fragments (out = k), files (out = nf + f)
+    std::vector<ShaDesc> sha, psha, ptw, gfr;  // per pass: fragments (out = k), files (out = nf + f); twins
     std::vector<uint64_t> job0(npass + 1, 0), desc0(npass + 1, 0), tiles(npass);
-    std::vector<uint32_t> prio(npass);
+    std::vector<uint32_t> prio(npass), nlanes(npass);
     std::vector<uint64_t> off(nfrag), len(nfrag);
+    // SHA lanes of pass p: each file's fileId part, with the group's fragments
+    // that sit on its block grid as twins (twins only if the launch stays
+    // above kChainMaxLanes lanes).
+    auto pass_lanes = [&](uint32_t p, bool twins) {
+        psha.clear();
+        ptw.clear();
+        for (uint32_t f = 0; f < nfiles; ++f) {
+            if (status[f] != DFS_OK) continue;
+            split(file_len[f], nfrag, off.data(), len.data());
+            gfr.clear();
+            for (uint32_t i = gb[p]; i < gb[p + 1]; ++i)
+                gfr.push_back(msg(file_off[f] + off[i], len[i], static_cast<uint64_t>(f) * nfrag + i));
+            const bool first = p == 0, last = p + 1 == npass;
+            const uint64_t a = first ? 0 : off[gb[p]] & ~63ull, e = last ? file_len[f] : off[gb[p + 1]] & ~63ull;
+            ShaDesc d = msg(file_off[f] + a, e - a, nf + f);
+            d.total = file_len[f];
+            d.flags = (first ? 0u : dfs::kShaResume) | (last ? 0u : dfs::kShaPartial);
+            add_lane_with_twins(psha, ptw, d, gfr.data(), static_cast<uint32_t>(gfr.size()), twins);
+        }
+    };
     for (uint32_t p = 0; p < npass; ++p) {
         pjobs.clear();
         items.clear();
-        psha.clear();
         for (uint32_t f = 0; f < nfiles; ++f) {
             if (status[f] != DFS_OK) continue;
             split(file_len[f], nfrag, off.data(), len.data());
@@ -1148,23 +1227,20 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
                 j.id = static_cast<uint32_t>(k);
                 pjobs.push_back(j);
                 items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
-                psha.push_back(msg(file_off[f] + off[i], len[i], k));
             }
-            const bool first = p == 0, last = p + 1 == npass;
-            const uint64_t a = first ? 0 : off[gb[p]] & ~63ull, e = last ? file_len[f] : off[gb[p + 1]] & ~63ull;
-            ShaDesc d = msg(file_off[f] + a, e - a, nf + f);
-            d.total = file_len[f];
-            d.flags = (first ? 0u : dfs::kShaResume) | (last ? 0u : dfs::kShaPartial);
-            psha.push_back(d);
         }
+        pass_lanes(p, true);
+        if (!ptw.empty() && psha.size() <= dfs::kChainMaxLanes) pass_lanes(p, false);
         tiles[p] = finish_jobs(pjobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
         prio[p] = sort_lanes(psha);  // one message per lane, longest first
         // Long items (balanced per SIMD, sha256_body): the fileId parts, which
         // are |group| fragments long; in a one-fragment pass every lane is
         // about one fragment long, so every item counts as long.
         if (pipe) prio[p] = static_cast<uint32_t>(gb[p + 1] - gb[p] == 1 ? psha.size() : nok);
+        nlanes[p] = static_cast<uint32_t>(psha.size());
         jobs.insert(jobs.end(), pjobs.begin(), pjobs.end());
         sha.insert(sha.end(), psha.begin(), psha.end());
+        sha.insert(sha.end(), ptw.begin(), ptw.end());
         job0[p + 1] = jobs.size();
         desc0[p + 1] = sha.size();
     }
@@ -1186,8 +1262,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(jobs.size()), tiles[0], d_out, d_st, nullptr, s));
         tm.end(DFS_T_B64DEC, s);
         tm.begin(DFS_T_SHA, s);
-        HIPC(dfs::launch_sha256(d_out, d_desc, static_cast<uint32_t>(sha.size()), nout, prio[0], d_dig, d_dig, d_queue,
-                                c->sha_wps, s));
+        HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
         tm.end(DFS_T_SHA, s);
     } else {
         HIPC(c->buf[B_DIG1].ensure(32ull * nout));  // running fileId states
@@ -1208,8 +1283,8 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         for (uint32_t p = 0; p < npass; ++p) {
             HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[p], 0));
             if (p == 0) tm.begin(DFS_T_SHA, c->aux);
-            HIPC(dfs::launch_sha256(d_out, d_desc + desc0[p], static_cast<uint32_t>(desc0[p + 1] - desc0[p]), nout,
-                                    prio[p], d_dig, d_dig, d_queue, c->sha_wps_beside, c->aux, d_state));
+            HIPC(dfs::launch_sha256(d_out, d_desc + desc0[p], nlanes[p], nout, prio[p], d_dig, d_dig, d_queue,
+                                    c->sha_wps_beside, c->aux, d_state));
         }
         tm.end(DFS_T_SHA, c->aux);
         HIPC(hipEventRecord(c->join, c->aux));

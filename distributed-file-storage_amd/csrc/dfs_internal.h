@@ -30,6 +30,14 @@ constexpr uint32_t kShaPartial = 2u;
 // kShaB64: also write the RFC 4648 Base64 of the message at b64out + b64
 // (fused upload encode; whole messages only, never with Resume/Partial).
 constexpr uint32_t kShaB64 = 4u;
+// kShaTwin (persistent kernel, plain instantiation only): the lane also
+// hashes `count` whole "twin" messages that start on its own 64-byte block
+// grid and lie inside its full blocks (a file's fragments that start at a
+// multiple of 64 bytes, e.g. fragment 0, or every fragment of a 256 KiB / N=8
+// file).  b64 = count << 32 | first: the twins are descs[n + first ...] (n =
+// the launch's lane count), in block order.  A twin block is loaded and its
+// message schedule expanded once for both states (sha256.hip compress2).
+constexpr uint32_t kShaTwin = 8u;
 
 // One byte-stream job for the tiled HBM-bound kernels (Base64 encode/decode,
 // gather, synth).  Jobs are sorted by tile_start; a sentinel job with
@@ -116,6 +124,10 @@ struct BodyParse {
 // `queue` is kShaQueueBytes of device memory, zeroed by the launcher on `s`
 // before a persistent launch; its grid holds waves_per_simd waves on each of
 // the 1024 SIMDs (fewer for small batches).
+// Lanes flagged kShaTwin need the persistent plain kernel: the host builds
+// twins only for launches of more than kChainMaxLanes lanes without b64
+// (add_lane_with_twins in dfs_gpu.cpp); the descriptor array then holds the
+// n lanes followed by their twins.
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
                          int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr);

@@ -73,6 +73,36 @@ __device__ __forceinline__ void compress(uint32_t (&st)[8], uint32_t (&W)[16]) {
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+// The same block W compressed into two independent states (a lane and its
+// twin, kShaTwin): the message schedule W[16..63] and K[t] + W[t] are
+// computed once, the two round chains interleave (2 x 14 ops per round +
+// 10 per schedule word + 1: ~2,290 VALU ops for two blocks instead of 2,810).
+__device__ __forceinline__ void compress2(uint32_t (&s1)[8], uint32_t (&s2)[8], uint32_t (&W)[16]) {
+    uint32_t a = s1[0], b = s1[1], c = s1[2], d = s1[3], e = s1[4], f = s1[5], g = s1[6], h = s1[7];
+    uint32_t a2 = s2[0], b2 = s2[1], c2 = s2[2], d2 = s2[3], e2 = s2[4], f2 = s2[5], g2 = s2[6], h2 = s2[7];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+        if (t >= 16) {
+            W[t & 15] += ssig1(W[(t - 2) & 15]) + W[(t - 7) & 15] + ssig0(W[(t - 15) & 15]);
+            asm volatile("" : "+v"(W[t & 15]));
+        }
+        const uint32_t kw = kK[t] + W[t & 15];
+        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
+        const uint32_t t2 = bsig0(a) + maj(a, b, c);
+        const uint32_t u1 = h2 + bsig1(e2) + ch(e2, f2, g2) + kw;
+        const uint32_t u2 = bsig0(a2) + maj(a2, b2, c2);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + t2;
+        h2 = g2; g2 = f2; f2 = e2; e2 = d2 + u1;
+        d2 = c2; c2 = b2; b2 = a2; a2 = u1 + u2;
+        asm volatile("" : "+v"(a), "+v"(e), "+v"(a2), "+v"(e2));
+    }
+    s1[0] += a; s1[1] += b; s1[2] += c; s1[3] += d;
+    s1[4] += e; s1[5] += f; s1[6] += g; s1[7] += h;
+    s2[0] += a2; s2[1] += b2; s2[2] += c2; s2[3] += d2;
+    s2[4] += e2; s2[5] += f2; s2[6] += g2; s2[7] += h2;
+}
+
 // 16 words of block k plus the look-ahead word (first word of block k+1),
 // which the unaligned funnel needs for the block's last word.
 __device__ __forceinline__ void load_block(const uint32_t* __restrict__ p, uint32_t sh, uint32_t (&r)[16],
@@ -160,6 +190,69 @@ __device__ __forceinline__ void store_digest(const uint32_t (&st)[8], uint32_t o
 __device__ __forceinline__ void init_state(uint32_t (&st)[8]) {
     st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
     st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
+}
+
+// Full blocks [kb, ke) of m (kb < ke) into st.  Blocks are fetched in pairs
+// (2j, 2j+1) requested back to back — one 128-byte line for line-aligned
+// messages, so L2 never has to keep a half-read line across a compression —
+// and the next pair is in flight while the current pair is compressed (two
+// pairs of register buffers, loop unrolled x4).  Beside the Base64 stream
+// this cut the SHA kernel's re-reads and its stalls on loaded HBM
+// (DESIGN.md §3.1).
+__device__ __forceinline__ void plain_range(uint32_t (&st)[8], const Msg& m, uint32_t kb, uint32_t ke) {
+    uint32_t A[16], B[16], C[16], D[16], xa, xb, xc, xd;
+    const uint32_t last = ke - 1u;
+    load_block(m.p + 16u * kb, m.sh, A, xa);
+    load_block(m.p + 16u * min(kb + 1u, last), m.sh, B, xb);
+    uint32_t k = kb;
+    for (;;) {
+        load_block(m.p + 16u * min(k + 2u, last), m.sh, C, xc);
+        load_block(m.p + 16u * min(k + 3u, last), m.sh, D, xd);
+        to_be(A, xa, m.sel);
+        compress(st, A);
+        if (++k >= ke) break;
+        to_be(B, xb, m.sel);
+        compress(st, B);
+        if (++k >= ke) break;
+        load_block(m.p + 16u * min(k + 2u, last), m.sh, A, xa);
+        load_block(m.p + 16u * min(k + 3u, last), m.sh, B, xb);
+        to_be(C, xc, m.sel);
+        compress(st, C);
+        if (++k >= ke) break;
+        to_be(D, xd, m.sel);
+        compress(st, D);
+        if (++k >= ke) break;
+    }
+}
+
+// Full blocks [kb, ke) of m into st and, from the same loads and schedule,
+// into the twin state s2 (kShaTwin).  Same pair fetch; unrolled x2 with a
+// register copy (a twin step is ~2,290 ops, so the copy costs < 1 %, and the
+// loop stays ~30 KB of code beside plain_range's ~45 KB).
+__device__ __forceinline__ void twin_range(uint32_t (&st)[8], uint32_t (&s2)[8], const Msg& m, uint32_t kb,
+                                           uint32_t ke) {
+    uint32_t A[16], B[16], C[16], D[16], xa, xb, xc, xd;
+    const uint32_t last = ke - 1u;
+    load_block(m.p + 16u * kb, m.sh, A, xa);
+    load_block(m.p + 16u * min(kb + 1u, last), m.sh, B, xb);
+    uint32_t k = kb;
+    for (;;) {
+        load_block(m.p + 16u * min(k + 2u, last), m.sh, C, xc);
+        load_block(m.p + 16u * min(k + 3u, last), m.sh, D, xd);
+        to_be(A, xa, m.sel);
+        compress2(st, s2, A);
+        if (++k >= ke) break;
+        to_be(B, xb, m.sel);
+        compress2(st, s2, B);
+        if (++k >= ke) break;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            A[i] = C[i];
+            B[i] = D[i];
+        }
+        xa = xc;
+        xb = xd;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -486,36 +579,41 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                     const uint64_t start = 64ull * m.nfull - m.nfull % 3u;
                     enc_tail(pair, base + descs[gid].off, start, m.len, b64 + descs[gid].b64);
                 }
-            } else if (m.nfull) {
-                // Blocks are fetched in pairs (2j, 2j+1) requested back to
-                // back — one 128-byte line for line-aligned messages, so L2
-                // never has to keep a half-read line across a compression —
-                // and the next pair is in flight while the current pair is
-                // compressed (two pairs of register buffers, loop unrolled
-                // x4).  Beside the Base64 stream this cut the SHA kernel's
-                // re-reads and its stalls on loaded HBM.
-                uint32_t A[16], B[16], C[16], D[16], xa, xb, xc, xd;
-                const uint32_t last = m.nfull - 1u;
-                load_block(m.p, m.sh, A, xa);
-                load_block(m.p + 16u * min(1u, last), m.sh, B, xb);
+            } else {
+                // Segments of the lane's full blocks: plain blocks up to the
+                // next twin's first block, then the twin's blocks with both
+                // states, the twin's own tail block(s) and digest, and so on.
+                // A lane without twins runs plain_range(0, nfull) once.
+                uint32_t tw = 0, tw_end = 0;
+                const uint64_t off0 = descs[gid].off;
+                if (m.flags & kShaTwin) {
+                    const uint64_t t = descs[gid].b64;
+                    tw = n + static_cast<uint32_t>(t);
+                    tw_end = tw + static_cast<uint32_t>(t >> 32);
+                }
                 uint32_t k = 0;
                 for (;;) {
-                    load_block(m.p + 16u * min(k + 2u, last), m.sh, C, xc);
-                    load_block(m.p + 16u * min(k + 3u, last), m.sh, D, xd);
-                    to_be(A, xa, m.sel);
-                    compress(st, A);
-                    if (++k >= m.nfull) break;
-                    to_be(B, xb, m.sel);
-                    compress(st, B);
-                    if (++k >= m.nfull) break;
-                    load_block(m.p + 16u * min(k + 2u, last), m.sh, A, xa);
-                    load_block(m.p + 16u * min(k + 3u, last), m.sh, B, xb);
-                    to_be(C, xc, m.sel);
-                    compress(st, C);
-                    if (++k >= m.nfull) break;
-                    to_be(D, xd, m.sel);
-                    compress(st, D);
-                    if (++k >= m.nfull) break;
+                    const bool has = tw < tw_end;
+                    uint32_t k0 = m.nfull;
+                    ShaDesc td{};
+                    if (has) {
+                        td = descs[tw];
+                        k0 = static_cast<uint32_t>((td.off - off0) >> 6);
+                    }
+                    if (k < k0) plain_range(st, m, k, k0);
+                    if (!has) break;
+                    const Msg t = msg_setup(base, td);
+                    uint32_t s2[8];
+                    init_state(s2);
+                    twin_range(st, s2, m, k0, k0 + t.nfull);
+                    for (uint32_t tb = 0; tb < t.ntb; ++tb) {
+                        uint32_t W[16];
+                        tail_block(t, tb, W);
+                        compress(s2, W);
+                    }
+                    store_digest(s2, t.out, split, out0, out1);
+                    k = k0 + t.nfull;
+                    ++tw;
                 }
             }
             if (m.flags & kShaPartial) {  // message continues in a later launch
