@@ -274,23 +274,14 @@ __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const 
 // each with one dwordx4 store at a 16-byte aligned address (a wave writes
 // 1 KiB contiguous per instruction).  Head, tail and final unit: dec_tail,
 // on wave 0 of the message's last tile.  Loads and stores are non-temporal.
-__global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
-                                                                  const StreamJob* __restrict__ jobs,
-                                                                  uint32_t njobs, uint64_t ntiles,
-                                                                  uint8_t* __restrict__ out,
-                                                                  int32_t* __restrict__ status,
-                                                                  uint64_t* __restrict__ out_len, uint32_t prio) {
-    if (prio) __builtin_amdgcn_s_setprio(3);  // beside the SHA kernel (pipelined download)
+// dec_range decodes tiles [t0, t1) of the job table.
+__device__ __forceinline__ void dec_range(const uint8_t* __restrict__ lut, uint32_t* __restrict__ stream,
+                                          const char* __restrict__ in, const StreamJob* __restrict__ jobs,
+                                          uint32_t njobs, uint8_t* __restrict__ out, int32_t* __restrict__ status,
+                                          uint64_t* __restrict__ out_len, uint64_t t0, uint64_t t1) {
     constexpr int GPL = kDecGpl;
     constexpr uint32_t kGroups = GPL * kStreamBlock;  // 4-unit groups per tile
     constexpr uint32_t kChunks = 3 * GPL * 64;        // 16-byte output chunks per tile (12 kGroups / 16)
-    __shared__ uint8_t lut[256];
-    __shared__ uint32_t stream[kGroups * 3 + 4];  // decoded bytes of the tile (+1 unit)
-    build_dec_lut(lut);
-    __syncthreads();
-
-    uint64_t t0, t1;
-    tile_range(ntiles, t0, t1);
     if (t0 >= t1) return;
     uint32_t j = find_job(jobs, njobs, t0);
     for (uint64_t t = t0; t < t1; ++t) {
@@ -356,6 +347,44 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
     }
 }
 
+template <bool AHEAD>
+__global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __restrict__ in,
+                                                                  const StreamJob* __restrict__ jobs,
+                                                                  uint32_t njobs, uint64_t ntiles,
+                                                                  uint8_t* __restrict__ out,
+                                                                  int32_t* __restrict__ status,
+                                                                  uint64_t* __restrict__ out_len, uint32_t prio,
+                                                                  const uint64_t* __restrict__ gtile, uint32_t ngroups,
+                                                                  uint32_t* __restrict__ gdone) {
+    if (prio) __builtin_amdgcn_s_setprio(3);  // beside the SHA kernel (pipelined / overlapped download)
+    constexpr uint32_t kGroups = kDecGpl * kStreamBlock;
+    __shared__ uint8_t lut[256];
+    __shared__ uint32_t stream[kGroups * 3 + 4];  // decoded bytes of the tile (+1 unit)
+    build_dec_lut(lut);
+    __syncthreads();
+
+    if (!AHEAD) {
+        uint64_t t0, t1;
+        tile_range(ntiles, t0, t1);
+        dec_range(lut, stream, in, jobs, njobs, out, status, out_len, t0, t1);
+        return;
+    }
+    // Decode-ahead (dfs_download_batch, overlap mode): fragment groups in
+    // order — every workgroup decodes its share of group g's tiles
+    // [gtile[g], gtile[g+1]), then publishes it: its stores drained and
+    // written back to memory at agent scope (release) before one lane adds 1
+    // to gdone[g].  The SHA kernel beside it reads group g once gdone[g]
+    // equals the grid size (then acquires).  This kernel never waits.
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    for (uint32_t g = 0; g < ngroups; ++g) {
+        const uint64_t a = gtile[g], n = gtile[g + 1] - a;
+        dec_range(lut, stream, in, jobs, njobs, out, status, out_len, a + n * b / G, a + n * (b + 1) / G);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(gdone + g, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 }  // namespace
 
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, char* out,
@@ -367,10 +396,16 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 }
 
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
-                             int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t prio, uint32_t wgs_per_cu) {
+                             int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t prio, uint32_t wgs_per_cu,
+                             const DecAhead* ahead) {
+    if (ahead) {  // every workgroup takes part in every group (gdone counts workgroups)
+        hipLaunchKernelGGL(b64_decode_kernel<true>, dim3(ahead->grid), dim3(kStreamBlock), 0, s, in, jobs, njobs, ntiles,
+                           out, status, out_len, prio, ahead->gtile, ahead->ngroups, ahead->gdone);
+        return hipGetLastError();
+    }
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(b64_decode_kernel, dim3(stream_grid(ntiles, wgs_per_cu)), dim3(kStreamBlock), 0, s, in, jobs, njobs, ntiles,
-                       out, status, out_len, prio);
+    hipLaunchKernelGGL(b64_decode_kernel<false>, dim3(stream_grid(ntiles, wgs_per_cu)), dim3(kStreamBlock), 0, s, in,
+                       jobs, njobs, ntiles, out, status, out_len, prio, nullptr, 0u, nullptr);
     return hipGetLastError();
 }
 

@@ -67,11 +67,15 @@ struct dfs_ctx {
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
     int sha_wps_beside = 3;      // ... when the Base64 kernel runs beside it (4 x 116 VGPRs leave no room)
     int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels (DFS_UPLOAD_MODE)
-    int download_mode = 0;       // 0 pipelined by fragment (decode || SHA), 1 decode then SHA (DFS_DOWNLOAD_MODE)
+    int download_mode = 2;       // 2 decode-ahead (one SHA launch waits per fragment group), 0 pipelined passes,
+                                 // 1 decode then SHA (DFS_DOWNLOAD_MODE=overlap|pipelined|serial)
+    int ovl_sha_wps = 2;         // overlap: SHA waves per SIMD (2 x 152 VGPRs + decode waves fit; DFS_OVL_SHA_WPS)
+    uint32_t ovl_dec_wgs = 2;    // overlap: decode workgroups per CU beside the SHA kernel (DFS_OVL_DEC_WGS)
     int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     uint32_t dec_prio = 1;       // decode waves at s_setprio 3 beside SHA (DFS_DEC_PRIO=0: 0)
     uint32_t dec_wgs = 1;        // decode workgroups per CU beside SHA (DFS_DEC_WGS)
+    uint64_t ovl_redo = 0;       // overlap downloads whose SHA launch was redone (a wait timed out)
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
     hipEvent_t fork = nullptr, join = nullptr;  // SHA || Base64 on two streams
@@ -365,7 +369,11 @@ int dfs_open(dfs_ctx** out, int device) {
     c->device = device;
     if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = c->sha_wps_beside = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_UPLOAD_MODE")) c->upload_mode = std::strcmp(w, "fused") == 0 ? 0 : 1;
-    if (const char* w = std::getenv("DFS_DOWNLOAD_MODE")) c->download_mode = std::strcmp(w, "serial") == 0 ? 1 : 0;
+    if (const char* w = std::getenv("DFS_DOWNLOAD_MODE"))
+        c->download_mode = std::strcmp(w, "serial") == 0 ? 1 : (std::strcmp(w, "pipelined") == 0 ? 0 : 2);
+    if (const char* w = std::getenv("DFS_OVL_SHA_WPS")) c->ovl_sha_wps = std::max(1, std::min(3, std::atoi(w)));
+    if (const char* w = std::getenv("DFS_OVL_DEC_WGS"))
+        c->ovl_dec_wgs = static_cast<uint32_t>(std::max(1, std::min(4, std::atoi(w))));
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     if (const char* w = std::getenv("DFS_DEC_PRIO")) c->dec_prio = std::atoi(w) ? 1u : 0u;
@@ -432,6 +440,13 @@ int dfs_get_timings(dfs_ctx* c, float* ms, int n) {
         HIPC(hipEventSynchronize(c->ev[2 * k + 1]));
         HIPC(hipEventElapsedTime(&ms[k], c->ev[2 * k], c->ev[2 * k + 1]));
     }
+    return DFS_OK;
+}
+
+int dfs_get_stats(dfs_ctx* c, uint64_t* out, int n) {
+    if (!c || !out) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    for (int k = 0; k < n; ++k) out[k] = k == DFS_S_OVL_REDO ? c->ovl_redo : 0;
     return DFS_OK;
 }
 
@@ -1172,7 +1187,13 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         d_out = c->buf[B_DATA_OUT].as<uint8_t>();
     }
     // Decode jobs write straight into the file at the split offsets (fused gather).
-    // Large batches run in passes over fragment groups {0}, {1, 2}, {3..6}, ...:
+    // Large batches, default (overlap): the decode runs fragment by fragment
+    // (group g = fragment g of every file): group 0 alone at full width, then
+    // groups 1.. beside ONE SHA launch over every lane (fileIds whole, twins),
+    // which waits in-kernel for each group's completion count (ShaWait,
+    // dfs_internal.h; bounded, the SHA launch is redone after the decode if a
+    // wait ever times out).  Pipelined (DFS_DOWNLOAD_MODE=pipelined): passes
+    // over fragment groups {0}, {1, 2}, {3..6}, ...:
     // pass p decodes its group of every file on s while the aux stream hashes
     // pass p - 1's fragments and advances every fileId over them (state in
     // HBM between launches, kShaResume / kShaPartial), so the SHA starts after
@@ -1181,30 +1202,35 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     // the last 64-byte boundary inside its group, so it reads decoded bytes only.
     uint64_t nok = 0;
     for (uint32_t f = 0; f < nfiles; ++f) nok += status[f] == DFS_OK;
-    const bool pipe = c->download_mode == 0 && nfrag > 1 && nok * (nfrag + 1) > dfs::kChainMaxLanes;
-    std::vector<uint32_t> gb{0};  // group p = fragments [gb[p], gb[p + 1])
-    for (uint32_t w = 1; gb.back() < nfrag; w *= 2) gb.push_back(pipe ? std::min(nfrag, gb.back() + w) : nfrag);
+    const bool big = nfrag > 1 && nok * (nfrag + 1) > dfs::kChainMaxLanes;
+    const bool ovl = big && c->download_mode == 2 && nfrag <= dfs::kShaWaitMaxGroups;
+    const bool pipe = big && c->download_mode == 0;
+    std::vector<uint32_t> gb{0};  // decode group p = fragments [gb[p], gb[p + 1])
+    for (uint32_t w = 1; gb.back() < nfrag; w *= 2)
+        gb.push_back(ovl ? gb.back() + 1 : (pipe ? std::min(nfrag, gb.back() + w) : nfrag));
     const uint32_t npass = static_cast<uint32_t>(gb.size() - 1);
+    const uint32_t nsha = ovl ? 1 : npass;  // SHA launches (overlap: one over every lane)
     std::vector<StreamJob> jobs, pjobs;
     std::vector<uint64_t> items;
     std::vector<ShaDesc> sha, psha, ptw, gfr;  // per pass: fragments (out = k), files (out = nf + f); twins
-    std::vector<uint64_t> job0(npass + 1, 0), desc0(npass + 1, 0), tiles(npass);
-    std::vector<uint32_t> prio(npass), nlanes(npass);
+    std::vector<uint64_t> job0(npass + 1, 0), desc0(nsha + 1, 0), tiles(npass);
+    std::vector<uint32_t> prio(nsha), nlanes(nsha);
     std::vector<uint64_t> off(nfrag), len(nfrag);
-    // SHA lanes of pass p: each file's fileId part, with the group's fragments
-    // that sit on its block grid as twins (twins only if the launch stays
-    // above kChainMaxLanes lanes).
+    // SHA lanes of launch p (fragments [i0, i1)): each file's fileId part,
+    // with the fragments that sit on its block grid as twins (twins only if
+    // the launch stays above kChainMaxLanes lanes).
     auto pass_lanes = [&](uint32_t p, bool twins) {
+        const uint32_t i0 = ovl ? 0 : gb[p], i1 = ovl ? nfrag : gb[p + 1];
         psha.clear();
         ptw.clear();
         for (uint32_t f = 0; f < nfiles; ++f) {
             if (status[f] != DFS_OK) continue;
             split(file_len[f], nfrag, off.data(), len.data());
             gfr.clear();
-            for (uint32_t i = gb[p]; i < gb[p + 1]; ++i)
+            for (uint32_t i = i0; i < i1; ++i)
                 gfr.push_back(msg(file_off[f] + off[i], len[i], static_cast<uint64_t>(f) * nfrag + i));
-            const bool first = p == 0, last = p + 1 == npass;
-            const uint64_t a = first ? 0 : off[gb[p]] & ~63ull, e = last ? file_len[f] : off[gb[p + 1]] & ~63ull;
+            const bool first = p == 0, last = p + 1 == nsha;
+            const uint64_t a = first ? 0 : off[i0] & ~63ull, e = last ? file_len[f] : off[i1] & ~63ull;
             ShaDesc d = msg(file_off[f] + a, e - a, nf + f);
             d.total = file_len[f];
             d.flags = (first ? 0u : dfs::kShaResume) | (last ? 0u : dfs::kShaPartial);
@@ -1229,23 +1255,47 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
                 items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
             }
         }
+        tiles[p] = finish_jobs(pjobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
+        jobs.insert(jobs.end(), pjobs.begin(), pjobs.end());
+        job0[p + 1] = jobs.size();
+        if (p >= nsha) continue;
         pass_lanes(p, true);
         if (!ptw.empty() && psha.size() <= dfs::kChainMaxLanes) pass_lanes(p, false);
-        tiles[p] = finish_jobs(pjobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
         prio[p] = sort_lanes(psha);  // one message per lane, longest first
         // Long items (balanced per SIMD, sha256_body): the fileId parts, which
         // are |group| fragments long; in a one-fragment pass every lane is
         // about one fragment long, so every item counts as long.
         if (pipe) prio[p] = static_cast<uint32_t>(gb[p + 1] - gb[p] == 1 ? psha.size() : nok);
         nlanes[p] = static_cast<uint32_t>(psha.size());
-        jobs.insert(jobs.end(), pjobs.begin(), pjobs.end());
         sha.insert(sha.end(), psha.begin(), psha.end());
         sha.insert(sha.end(), ptw.begin(), ptw.end());
-        job0[p + 1] = jobs.size();
         desc0[p + 1] = sha.size();
+    }
+    // Overlap: groups 1.. as one job table with continuous tile numbers
+    // (jobs2, after the per-group tables in B_JOBS) and group bounds gtile.
+    std::vector<uint64_t> gtile;
+    uint64_t job2 = 0;
+    if (ovl) {
+        job2 = jobs.size();
+        uint64_t t = 0;
+        for (uint32_t p = 1; p < npass; ++p) {
+            gtile.push_back(t);
+            for (uint64_t j = job0[p]; j + 1 < job0[p + 1]; ++j) {  // without the group's sentinel
+                StreamJob x = jobs[j];
+                x.tile_start += t;
+                jobs.push_back(x);
+            }
+            t += tiles[p];
+        }
+        gtile.push_back(t);
+        StreamJob sent{};
+        sent.tile_start = t;
+        jobs.push_back(sent);
     }
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
+    if (ovl)
+        if (int rc = put(c, B_JOBS2, gtile.data(), gtile.size() * sizeof(uint64_t), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * nf));
     HIPC(c->buf[B_DIG0].ensure(32ull * (nf + nfiles)));
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
@@ -1257,7 +1307,36 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     uint32_t* d_queue = c->buf[B_QUEUE].as<uint32_t>();
     const uint32_t nout = static_cast<uint32_t>(nf + nfiles);
     tm.begin(DFS_T_TOTAL, s);
-    if (!pipe) {
+    if (ovl) {
+        if (!c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        if (c->pass_ev.empty()) {
+            hipEvent_t ev = nullptr;
+            HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            c->pass_ev.push_back(ev);
+        }
+        // The counters live in the SHA queue words, zeroed here (before the
+        // decode that publishes them; the SHA launch does not re-zero them).
+        HIPC(hipMemsetAsync(d_queue, 0, dfs::kShaQueueBytes, s));
+        tm.begin(DFS_T_B64DEC, s);
+        HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(job0[1]), tiles[0], d_out, d_st, nullptr, s));
+        HIPC(hipEventRecord(c->pass_ev[0], s));
+        dfs::DecAhead ah{c->buf[B_JOBS2].as<uint64_t>(), npass - 1, 256u * c->ovl_dec_wgs,
+                         d_queue + dfs::kShaWaitSlot + 1};
+        HIPC(dfs::launch_b64_decode(d_in, d_jobs + job2, static_cast<uint32_t>(jobs.size() - job2), gtile.back(), d_out,
+                                    d_st, nullptr, s, c->dec_prio, 0, &ah));
+        tm.end(DFS_T_B64DEC, s);
+        // The SHA launch waits for group 0 by stream order and for groups
+        // 1.. in-kernel.  Launched after the decode it waits on, and sized to
+        // leave room for the decode waves, so the decode always progresses.
+        HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[0], 0));
+        tm.begin(DFS_T_SHA, c->aux);
+        const dfs::ShaWait wt{d_queue + dfs::kShaWaitSlot, ah.grid, 1u, nfrag, static_cast<uint32_t>(nf)};
+        HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->ovl_sha_wps,
+                                c->aux, nullptr, nullptr, &wt));
+        tm.end(DFS_T_SHA, c->aux);
+        HIPC(hipEventRecord(c->join, c->aux));
+        HIPC(hipStreamWaitEvent(s, c->join, 0));
+    } else if (!pipe) {
         tm.begin(DFS_T_B64DEC, s);
         HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(jobs.size()), tiles[0], d_out, d_st, nullptr, s));
         tm.end(DFS_T_B64DEC, s);
@@ -1293,10 +1372,18 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(nf);
     std::vector<uint8_t> dig(32ull * (nf + nfiles));
+    uint32_t timed_out = 0;
+    if (ovl) HIPC(hipMemcpyAsync(&timed_out, d_queue + 2, 4, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * nf, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
     if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+    if (timed_out) {  // a decode-ahead wait gave up: hash again now that the decode is complete
+        ++c->ovl_redo;
+        HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
+        HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
     std::vector<uint8_t> expf, expd;
     if (dev && exp_frag && is_device_ptr(exp_frag)) {  // expected digests may live on the device in device mode
         expf.resize(32ull * nf);

@@ -124,13 +124,36 @@ struct BodyParse {
 // `queue` is kShaQueueBytes of device memory, zeroed by the launcher on `s`
 // before a persistent launch; its grid holds waves_per_simd waves on each of
 // the 1024 SIMDs (fewer for small batches).
+// Decode-ahead download (dfs_download_batch, overlap mode): the SHA kernel
+// runs beside the decode and reads fragment group g (fragment g of every
+// file) only after done[g] reached `target` (the decode grid size: every
+// decode workgroup adds 1 after publishing its share of g with an agent-scope
+// release; sha256.hip acquires).  Groups below `first` were decoded by an
+// earlier launch on the stream the SHA launch waits for.  Fragment lanes
+// (digest slot out < nf) read group out % nfrag; fileId lanes (out >= nf,
+// whole files split SN:138-157 into nfrag fragments) wait at each fragment's
+// first block.  A wait is bounded: past kShaWaitTicks the lane goes on, sets
+// queue[2] and the host re-runs the SHA launch after the decode.
+struct ShaWait {
+    const uint32_t* done;
+    uint32_t target, first, nfrag, nf;
+};
+constexpr uint32_t kShaWaitSlot = 8;  // done[g] = queue[kShaWaitSlot + g] (kShaQueueBytes)
+constexpr uint32_t kShaWaitMaxGroups = 48;
+struct DecAhead {
+    const uint64_t* gtile;  // group g = tiles [gtile[g], gtile[g + 1])
+    uint32_t ngroups, grid;
+    uint32_t* gdone;
+};
+
 // Lanes flagged kShaTwin need the persistent plain kernel: the host builds
 // twins only for launches of more than kChainMaxLanes lanes without b64
 // (add_lane_with_twins in dfs_gpu.cpp); the descriptor array then holds the
 // n lanes followed by their twins.
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
-                         int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr);
+                         int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr,
+                         const ShaWait* wait = nullptr);
 // Tiles hold kEncPer*256 12-byte groups (the job table's tile_start must be
 // built with that tile size); prio = s_setprio of the encode waves.
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
@@ -141,9 +164,11 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 // a different length sets status bit 2.  Tiles hold kDecGpl*256 4-unit groups.
 // prio != 0: the waves run at s_setprio 3 (beside the SHA kernel); the grid
 // holds at most wgs_per_cu persistent workgroups per CU.
+// ahead: decode-ahead mode (group order, per-group completion counters,
+// grid = ahead->grid workgroups); the tile count is then ahead->gtile's.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
                              uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t prio = 0,
-                             uint32_t wgs_per_cu = 8);
+                             uint32_t wgs_per_cu = 8, const DecAhead* ahead = nullptr);
 // Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
 hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
                                    hipStream_t s);

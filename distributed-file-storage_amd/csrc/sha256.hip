@@ -459,13 +459,44 @@ __device__ __forceinline__ uint32_t simd_key() {
 // ENC = the fused-Base64 instantiation (launched when the caller passes a
 // Base64 output; lanes flagged kShaB64 also write their message's Base64).
 constexpr uint32_t kStealSpins = 16;  // x s_sleep 127 (8,128 clocks each)
+constexpr uint64_t kShaWaitTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
-template <bool ENC>
+// Decode-ahead (ShaWait, dfs_internal.h): the active lanes of the wave wait
+// until fragment group `need` (per lane; ~0u = nothing to wait for) has been
+// published by every decode workgroup, then acquire at agent scope so the
+// loads that follow see the decoded bytes (the decode ran on other CUs / XCDs).
+// Bounded: on timeout queue[2] is set (the host re-runs the SHA launch after
+// the decode) and the lane goes on, so the grid always drains.
+__device__ __forceinline__ void wait_group(const ShaWait& w, uint32_t need, uint32_t* __restrict__ queue) {
+    const bool want = need != ~0u && need >= w.first;
+    bool ok = !want || __hip_atomic_load(w.done + need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= w.target;
+    if (__ballot(!ok)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            __builtin_amdgcn_s_sleep(32);
+            if (!ok) ok = __hip_atomic_load(w.done + need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= w.target;
+            if (!__ballot(!ok)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kShaWaitTicks) {
+                atomicOr(queue + 2, 1u);
+                break;
+            }
+        }
+    }
+    if (__ballot(want)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// First block of fragment g of a file of S bytes split into N (SN:138-157).
+__device__ __forceinline__ uint32_t frag_block(uint64_t S, uint32_t N, uint32_t g) {
+    const uint64_t base = S / N, rem = S % N;
+    return static_cast<uint32_t>((g * base + (g < rem ? g : rem)) >> 6);
+}
+
+template <bool ENC, bool WAIT>
 __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, const ShaDesc* __restrict__ descs,
                                             uint32_t n, uint32_t split, uint32_t n_long, uint32_t cap,
                                             uint8_t* __restrict__ out0, uint8_t* __restrict__ out1,
                                             uint32_t* __restrict__ queue, uint32_t* __restrict__ state,
-                                            char* __restrict__ b64) {
+                                            char* __restrict__ b64, const ShaWait& W) {
     const uint32_t nitems = (n + 63u) >> 6;
     const uint32_t n_short = nitems - n_long;
     const uint32_t lane = threadIdx.x & 63u;
@@ -584,6 +615,11 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                 // next twin's first block, then the twin's blocks with both
                 // states, the twin's own tail block(s) and digest, and so on.
                 // A lane without twins runs plain_range(0, nfull) once.
+                // With ShaWait (decode-ahead download) a segment also ends
+                // where the lane next has to wait for a fragment group: a
+                // fragment lane waits for its own group before its first
+                // block, a fileId lane for group g before the block holding
+                // fragment g's first byte (twins never straddle those).
                 uint32_t tw = 0, tw_end = 0;
                 const uint64_t off0 = descs[gid].off;
                 if (m.flags & kShaTwin) {
@@ -591,8 +627,26 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                     tw = n + static_cast<uint32_t>(t);
                     tw_end = tw + static_cast<uint32_t>(t >> 32);
                 }
+                uint32_t wg = 0, wn = 0, wb = ~0u;  // next group to wait for, groups end, its first block
+                if (WAIT) {
+                    if (m.out < W.nf) {
+                        wg = m.out % W.nfrag;
+                        wn = wg + 1;
+                    } else {
+                        wn = W.nfrag;
+                    }
+                    wb = 0;
+                }
                 uint32_t k = 0;
                 for (;;) {
+                    if (WAIT) {
+                        uint32_t need = ~0u;
+                        while (wg < wn && wb <= k) {
+                            need = wg++;
+                            wb = wg < wn ? (m.out < W.nf ? 0u : frag_block(m.total, W.nfrag, wg)) : ~0u;
+                        }
+                        wait_group(W, need, queue);
+                    }
                     const bool has = tw < tw_end;
                     uint32_t k0 = m.nfull;
                     ShaDesc td{};
@@ -600,7 +654,12 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                         td = descs[tw];
                         k0 = static_cast<uint32_t>((td.off - off0) >> 6);
                     }
-                    if (k < k0) plain_range(st, m, k, k0);
+                    const uint32_t ke = min(k0, wb);
+                    if (k < ke) {
+                        plain_range(st, m, k, ke);
+                        k = ke;
+                        continue;
+                    }
                     if (!has) break;
                     const Msg t = msg_setup(base, td);
                     uint32_t s2[8];
@@ -766,16 +825,22 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
 #define DFS_SHA_ARGS                                                                                     \
     const uint8_t *__restrict__ base, const ShaDesc *__restrict__ descs, uint32_t n, uint32_t split,       \
         uint32_t n_long, uint32_t cap, uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,             \
-        uint32_t *__restrict__ queue, uint32_t *__restrict__ state, char *__restrict__ b64
+        uint32_t *__restrict__ queue, uint32_t *__restrict__ state, char *__restrict__ b64, ShaWait wait
 // Plain (hash only).  The pair-fetch block loop measured 76.6 ms alone on
 // config 2 (78.8 ms with two register buffers, 79.4 ms with one compression
 // per iteration); beside Base64 91.3 / 93.1 / 93.9 ms.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes(DFS_SHA_ARGS) {
-    sha256_body<false>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64);
+    sha256_body<false, false>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64, wait);
+}
+// Decode-ahead download (ShaWait): lanes wait in-kernel for fragment groups.
+// Its own instantiation: the wait state costs VGPRs (157 vs 149), and the
+// upload's SHA waves must leave room for the Base64 waves beside them.
+__global__ __launch_bounds__(kShaBlock) void sha256_lanes_wait(DFS_SHA_ARGS) {
+    sha256_body<false, true>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64, wait);
 }
 // Fused: fragment lanes flagged kShaB64 also write their Base64.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
-    sha256_body<true>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64);
+    sha256_body<true, false>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64, wait);
 }
 #undef DFS_SHA_ARGS
 
@@ -783,15 +848,18 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
-                         hipStream_t s, uint32_t* state, char* b64) {
+                         hipStream_t s, uint32_t* state, char* b64, const ShaWait* wait) {
     if (n == 0) return hipSuccess;
-    if (!b64 && n <= kChainMaxLanes) {  // latency-bound launch: owner + helper waves
+    if (!b64 && !wait && n <= kChainMaxLanes) {  // latency-bound launch: owner + helper waves
         hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, split, out0,
                            out1, state);
         return hipGetLastError();
     }
-    hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
-    if (e != hipSuccess) return e;
+    const ShaWait wt = wait && !b64 ? *wait : ShaWait{};
+    if (!wait) {  // with a wait the caller zeroed the queue before the decode it waits on
+        hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
+        if (e != hipSuccess) return e;
+    }
     const uint32_t n_long = (prio_lanes + 63u) / 64u;
     const uint32_t cap = (n_long + 1023u) / 1024u;
     const uint64_t items = (n + 63u) / 64u;
@@ -800,10 +868,13 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     if (b64) {
         hipLaunchKernelGGL(sha256_lanes_b64, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
-                           out0, out1, queue, state, b64);
+                           out0, out1, queue, state, b64, ShaWait{});
+    } else if (wt.done) {
+        hipLaunchKernelGGL(sha256_lanes_wait, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
+                           out0, out1, queue, state, nullptr, wt);
     } else {
         hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
-                           out1, queue, state, nullptr);
+                           out1, queue, state, nullptr, wt);
     }
     return hipGetLastError();
 }

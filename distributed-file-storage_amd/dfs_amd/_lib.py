@@ -46,6 +46,7 @@ DFS_PLACE_RING, DFS_PLACE_STAR, DFS_PLACE_FETCH = 0, 1, 2
 DFS_XFER_SEND, DFS_XFER_RECV, DFS_XFER_COPY = 0, 1, 2
 
 DFS_T_SHA, DFS_T_B64ENC, DFS_T_B64DEC, DFS_T_GATHER, DFS_T_TOTAL, DFS_T_COUNT = range(6)
+DFS_S_OVL_REDO, DFS_S_COUNT = range(2)
 
 
 class dfs_span(ctypes.Structure):
@@ -84,6 +85,7 @@ SIGNATURES = {
     "dfs_set_stream": (_int, [_vp, _vp]),
     "dfs_set_profiling": (_int, [_vp, _int]),
     "dfs_get_timings": (_int, [_vp, _vp, _int]),
+    "dfs_get_stats": (_int, [_vp, _vp, _int]),
     "dfs_split_plan": (_int, [_u64, _u32, _vp]),
     "dfs_b64_encoded_len": (_u64, [_u64]),
     "dfs_b64_decoded_cap": (_u64, [_u64]),
@@ -156,6 +158,8 @@ def lib() -> ctypes.CDLL:
             pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("DFS_LIB_PATH") and not hasattr(L, name):
+                continue  # an older A/B build: its missing entry points stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

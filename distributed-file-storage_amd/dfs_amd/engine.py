@@ -117,6 +117,13 @@ class FragmentEngine:
         names = ["sha", "b64enc", "b64dec", "gather", "total"]
         return {k: (v if v >= 0 else None) for k, v in zip(names, ms)}
 
+    def stats(self) -> dict:
+        """ctx counters (dfs_get_stats): ovl_redo = decode-ahead downloads
+        whose SHA launch was redone after an in-kernel wait timed out."""
+        v = (ctypes.c_uint64 * L.DFS_S_COUNT)()
+        check(lib().dfs_get_stats(self._ctx, v, L.DFS_S_COUNT), "dfs_get_stats")
+        return {"ovl_redo": int(v[0])}
+
     # -- sha256Hex (SN:603-613) ----------------------------------------------
     def sha256(self, messages: Sequence[bytes]) -> List[bytes]:
         buf, spans = _pack(messages)

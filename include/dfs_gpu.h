@@ -97,6 +97,13 @@ int dfs_set_profiling(dfs_ctx* ctx, int on);
 #define DFS_T_TOTAL 4    /* whole call, first launch to last     */
 #define DFS_T_COUNT 5
 int dfs_get_timings(dfs_ctx* ctx, float* ms, int n);
+/* Counters of the ctx since dfs_open (diagnostics, no reference equivalent):
+ * DFS_S_OVL_REDO = decode-ahead downloads whose SHA launch was redone after
+ * the decode because an in-kernel wait for a fragment group timed out (the
+ * results are still exact; the call was slow). */
+#define DFS_S_OVL_REDO 0
+#define DFS_S_COUNT 1
+int dfs_get_stats(dfs_ctx* ctx, uint64_t* out, int n);
 
 /* ---- pure host helpers (no device) ---------------------------------------- */
 /* handleUpload's split (SN:138-171): fragment i has floor(S/N) + (i < S mod N)

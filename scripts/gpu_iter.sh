@@ -21,3 +21,13 @@ echo "== bench --config 3"
 timeout -k 10 400 python -u bench.py --config 3 --steps 5 --no-batcher --no-cpu-baseline --no-store --no-wire ${C3_ARGS} \
   > gpurun_out/bench_c3.json 2> gpurun_out/bench_c3.err || { tail -20 gpurun_out/bench_c3.err; fatal 9; }
 cat gpurun_out/bench_c3.json; grep "^\[bench\]" gpurun_out/bench_c3.err | tail -8
+# Same-box A/B of the upload step against an earlier build (AB_LIB=path).
+if [ -n "$AB_LIB" ]; then
+  for lib in "$AB_LIB" ""; do
+    echo "== A/B upload: ${lib:-this tree}"
+    DFS_LIB_PATH=$lib timeout -k 10 300 python -u bench.py --steps 10 --no-batcher --no-cpu-baseline --no-store --no-wire \
+      --no-download --frag-only-steps 0 --b64-steps 0 ${AB_ARGS} > gpurun_out/ab.json 2> gpurun_out/ab.err \
+      || { tail -20 gpurun_out/ab.err; fatal 10; }
+    python3 -c "import json;d=json.load(open('gpurun_out/ab.json'));print(d['ms_per_step'], d['roofline']['ms'], d['roofline']['frac'])"
+  done
+fi

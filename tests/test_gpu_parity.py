@@ -634,20 +634,23 @@ def test_sha256_both_kernels_large_and_small_launches(engine):
     assert all(small[i].tobytes() == want[i] for i in range(5000))
 
 
-@pytest.mark.parametrize("mode", ["pipelined", "serial"])
+@pytest.mark.parametrize("mode", ["overlap", "pipelined", "serial"])
 def test_download_overlapped_large_batch(engine, mode, monkeypatch):
     """A download above dfs::kChainMaxLanes SHA lanes.  6,000 files (36,000
     lanes): every file rebuilt and verified, plus the failure statuses on a
     few files — missing fragment (SN:443-446), invalid Base64 (SN:281), wrong
     fragment digest (SN:250-257), wrong fileId (SN:455-458), a Base64 char
     changed to another alphabet char (decodes, digest differs) — and their
-    neighbours unaffected.  Default: pipelined by fragment (pass i decodes
-    fragment i of every file while the fileIds advance over fragment i - 1,
-    their states in HBM between launches); DFS_DOWNLOAD_MODE=serial: the whole
-    decode, then one SHA launch.  One unpadded fragment (valid for the JDK
+    neighbours unaffected.  Default (overlap): fragment 0 of every file
+    decoded first, then the other fragments in order beside one SHA launch
+    whose lanes wait in-kernel for each fragment group;
+    DFS_DOWNLOAD_MODE=pipelined: passes by fragment group (pass i decodes its
+    group while the fileIds advance over group i - 1, their states in HBM
+    between launches); DFS_DOWNLOAD_MODE=serial: the whole decode, then one
+    SHA launch.  One unpadded fragment (valid for the JDK
     decoder) shifts every later Base64 offset off dword alignment."""
-    if mode == "serial":
-        monkeypatch.setenv("DFS_DOWNLOAD_MODE", "serial")
+    if mode != "overlap":
+        monkeypatch.setenv("DFS_DOWNLOAD_MODE", mode)
         engine = dfs_amd.FragmentEngine(0)
     import base64
     rng = np.random.default_rng(31)
@@ -677,8 +680,9 @@ def test_download_overlapped_large_batch(engine, mode, monkeypatch):
     texts[f][0] = texts[f][0].rstrip(b"=")
     try:
         res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+        assert engine.stats()["ovl_redo"] == 0  # no decode-ahead wait timed out
     finally:
-        if mode == "serial":
+        if mode != "overlap":
             engine.close()
     for f, (st, body) in enumerate(res):
         assert st == want[f], (f, st, want[f])
@@ -687,11 +691,17 @@ def test_download_overlapped_large_batch(engine, mode, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_download_pipelined_many_fragments_small_files(engine):
-    """The pipelined download with nfrag = 12 and small files: fileId parts of
-    0 bytes in most passes (files under 64 B per fragment), parts ending on
-    every 64-byte boundary case, empty files and fragments; 3,000 files x 13
-    lanes = 39,000 (above dfs::kChainMaxLanes, so the pipelined path)."""
+@pytest.mark.parametrize("mode", ["overlap", "pipelined"])
+def test_download_pipelined_many_fragments_small_files(engine, mode, monkeypatch):
+    """The pipelined / overlapped download with nfrag = 12 and small files:
+    fileId parts of 0 bytes in most passes (files under 64 B per fragment),
+    parts ending on every 64-byte boundary case, empty files and fragments;
+    fileId lanes whose wait points (each fragment's first block) coincide
+    (several fragments start inside one block); 3,000 files x 13 lanes =
+    39,000 (above dfs::kChainMaxLanes, so the large-batch paths)."""
+    if mode != "overlap":
+        monkeypatch.setenv("DFS_DOWNLOAD_MODE", mode)
+        engine = dfs_amd.FragmentEngine(0)
     import base64
     rng = np.random.default_rng(77)
     nfiles, nfrag = 3000, 12
@@ -705,7 +715,12 @@ def test_download_pipelined_many_fragments_small_files(engine):
         texts.append([base64.b64encode(p) for p in parts])
         frag_h.append([hashlib.sha256(p).hexdigest() for p in parts])
         file_h.append(hashlib.sha256(d).hexdigest())
-    res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+    try:
+        res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+        assert engine.stats()["ovl_redo"] == 0  # no decode-ahead wait timed out
+    finally:
+        if mode != "overlap":
+            engine.close()
     for f, (st, body) in enumerate(res):
         assert st == 0, (f, st)
         assert body == files[f], f

@@ -69,15 +69,17 @@ def test_twin_upload_ragged(engine):
     _check_upload(engine, _files(sizes, 6), 4)
 
 
-@pytest.mark.parametrize("mode", ["pipelined", "serial"])
+@pytest.mark.parametrize("mode", ["overlap", "pipelined", "serial"])
 @pytest.mark.parametrize("nfiles,size,nfrag", [(36000, 2048, 8), (40000, 1000, 5)])
 def test_twin_download(engine, mode, nfiles, size, nfrag, monkeypatch):
-    """Download of twin-shaped batches: pipelined (pass p's fileId part carries
-    the group's on-grid fragments as twins) and serial (one launch), every file
-    rebuilt and verified, plus a wrong fragment digest on a twin (fragment 0)
-    and on a non-twin, and a wrong fileId."""
-    if mode == "serial":
-        monkeypatch.setenv("DFS_DOWNLOAD_MODE", "serial")
+    """Download of twin-shaped batches: overlap (one SHA launch beside the
+    fragment-ordered decode; twins inside the fileId lane's wait segments),
+    pipelined (pass p's fileId part carries the group's on-grid fragments as
+    twins) and serial (one launch), every file rebuilt and verified, plus a
+    wrong fragment digest on a twin (fragment 0) and on a non-twin, and a
+    wrong fileId."""
+    if mode != "overlap":
+        monkeypatch.setenv("DFS_DOWNLOAD_MODE", mode)
         engine = dfs_amd.FragmentEngine(0)
     try:
         files = _files([size] * nfiles, 3 * nfiles + size)
@@ -95,8 +97,9 @@ def test_twin_download(engine, mode, nfiles, size, nfrag, monkeypatch):
         file_h[nfiles - 1] = "f" * 64
         want[nfiles - 1] = dfs_amd.DFS_E_CORRUPT
         res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
+        assert engine.stats()["ovl_redo"] == 0  # no decode-ahead wait timed out
     finally:
-        if mode == "serial":
+        if mode != "overlap":
             engine.close()
     for f, (st, body) in enumerate(res):
         assert st == want[f], f
