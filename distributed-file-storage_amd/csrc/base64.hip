@@ -387,6 +387,12 @@ __global__ __launch_bounds__(kStreamBlock) void b64_decode_kernel(const char* __
 
 }  // namespace
 
+int dec_ahead_vgprs() {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(b64_decode_kernel<true>)) == hipSuccess ? a.numRegs
+                                                                                                        : -1;
+}
+
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, char* out,
                              uint32_t wgs_per_cu, hipStream_t s, uint32_t prio) {
     if (ntiles == 0) return hipSuccess;

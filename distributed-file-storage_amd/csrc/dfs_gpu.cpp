@@ -69,8 +69,9 @@ struct dfs_ctx {
     int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels (DFS_UPLOAD_MODE)
     int download_mode = 2;       // 2 decode-ahead (one SHA launch waits per fragment group), 0 pipelined passes,
                                  // 1 decode then SHA (DFS_DOWNLOAD_MODE=overlap|pipelined|serial)
-    int ovl_sha_wps = 2;         // overlap: SHA waves per SIMD (2 x 152 VGPRs + decode waves fit; DFS_OVL_SHA_WPS)
-    uint32_t ovl_dec_wgs = 2;    // overlap: decode workgroups per CU beside the SHA kernel (DFS_OVL_DEC_WGS)
+    int ovl_sha_wps = 3;         // overlap: SHA waves per SIMD (DFS_OVL_SHA_WPS) ...
+    uint32_t ovl_dec_wgs = 1;    // ... and decode workgroups per CU beside them (DFS_OVL_DEC_WGS); both
+                                 // clamped at open so the two grids are resident together (ovl_fit)
     int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     uint32_t dec_prio = 1;       // decode waves at s_setprio 3 beside SHA (DFS_DEC_PRIO=0: 0)
@@ -201,8 +202,8 @@ uint32_t sort_lanes(std::vector<ShaDesc>& d) {
 // 64 (256 KiB files, N = 8: BASELINE configs[2]), every fragment.  Appends
 // `primary` (with its twin list) and the fragments that are not twins to
 // `lanes`, the twins to `tw` (launched as descs[n_lanes + ...]).  Twins need
-// the persistent kernel: callers enable them only for launches of more than
-// dfs::kChainMaxLanes lanes that run without the fused Base64.
+// the persistent kernel: callers keep them only for launches of at least
+// dfs::kTwinMinLanes lanes (> kChainMaxLanes) that run without the fused Base64.
 void add_lane_with_twins(std::vector<ShaDesc>& lanes, std::vector<ShaDesc>& tw, ShaDesc primary,
                          const ShaDesc* frags, uint32_t nfr, bool enable) {
     const uint64_t first = tw.size();
@@ -356,6 +357,23 @@ const char* dfs_strerror(int code) {
     }
 }
 
+// Decode-ahead download: every SHA wave may wait on every decode workgroup,
+// so both grids must be resident at once.  Per SIMD, wps SHA waves plus
+// dec_wgs decode waves (a 256-thread workgroup puts one wave on each SIMD of
+// its CU) must fit the 512-entry VGPR file (allocation granularity 8); LDS
+// (one ~25 KB decode workgroup per wave slot) and the 32 waves per CU are far
+// from their limits.  Fewer decode workgroups first, then fewer SHA waves.
+static void ovl_fit(dfs_ctx* c) {
+    const int sv = dfs::sha_wait_vgprs(), dv = dfs::dec_ahead_vgprs();
+    if (sv <= 0 || dv <= 0) return;  // attributes unavailable: keep the defaults
+    const int sa = (sv + 7) / 8 * 8, da = (dv + 7) / 8 * 8;
+    while (c->ovl_sha_wps * sa + static_cast<int>(c->ovl_dec_wgs) * da > 512) {
+        if (c->ovl_dec_wgs > 1) --c->ovl_dec_wgs;
+        else if (c->ovl_sha_wps > 1) --c->ovl_sha_wps;
+        else break;
+    }
+}
+
 int dfs_open(dfs_ctx** out, int device) {
     if (!out) return DFS_E_ARG;
     *out = nullptr;
@@ -374,6 +392,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_OVL_SHA_WPS")) c->ovl_sha_wps = std::max(1, std::min(3, std::atoi(w)));
     if (const char* w = std::getenv("DFS_OVL_DEC_WGS"))
         c->ovl_dec_wgs = static_cast<uint32_t>(std::max(1, std::min(4, std::atoi(w))));
+    ovl_fit(c);
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     if (const char* w = std::getenv("DFS_DEC_PRIO")) c->dec_prio = std::atoi(w) ? 1u : 0u;
@@ -812,7 +831,7 @@ int build_host_plan(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint
         }
     }
     build_all_lanes(files, nfiles, nfrag, h.frag, twins, h);
-    if (h.twins && h.n_all <= dfs::kChainMaxLanes) build_all_lanes(files, nfiles, nfrag, h.frag, false, h);
+    if (h.twins && h.n_all < dfs::kTwinMinLanes) build_all_lanes(files, nfiles, nfrag, h.frag, false, h);
     // Base64 layout: [file][fragment] (default) or [fragment][file].
     uint64_t total = 0;
     auto place = [&](uint32_t f, uint32_t i) {
@@ -1260,7 +1279,17 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         job0[p + 1] = jobs.size();
         if (p >= nsha) continue;
         pass_lanes(p, true);
-        if (!ptw.empty() && psha.size() <= dfs::kChainMaxLanes) pass_lanes(p, false);
+        if (!ptw.empty() && psha.size() < dfs::kTwinMinLanes) pass_lanes(p, false);
+        // Overlap: fragment lanes group-major (fragment 1 of every file, then
+        // fragment 2, ...; fileIds first) before the stable longest-first
+        // sort, so each 64-lane item waits for one group and the queue hands
+        // out items in decode order.  File-major items would hold fragments
+        // 1..N-1 of 16 files and wait for the last group.
+        if (ovl)
+            std::stable_sort(psha.begin(), psha.end(), [&](const ShaDesc& x, const ShaDesc& y) {
+                const uint32_t kx = x.out >= nf ? 0u : 1u + x.out % nfrag, ky = y.out >= nf ? 0u : 1u + y.out % nfrag;
+                return kx < ky;
+            });
         prio[p] = sort_lanes(psha);  // one message per lane, longest first
         // Long items (balanced per SIMD, sha256_body): the fileId parts, which
         // are |group| fragments long; in a one-fragment pass every lane is

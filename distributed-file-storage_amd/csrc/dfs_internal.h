@@ -58,6 +58,12 @@ constexpr size_t kShaQueueBytes = 4 * (64 + 8192);  // SHA queue words + per-SIM
 // at once) run the latency kernel sha256_chain; larger ones the persistent
 // throughput kernel sha256_lanes.
 constexpr uint32_t kChainMaxLanes = 32768;
+// Twin lanes (kShaTwin) are built only when the launch keeps at least one
+// wave of lanes per SIMD (1,024 SIMDs x 64): each twin lane is a whole file's
+// chain, so fewer lanes leave SIMDs idle and the plain split wins (e.g. a
+// 32,768-file chunk of 256 KiB files: 17.6 ms with twins on half the SIMDs
+// vs ~11.5 ms as 294,912 plain lanes).
+constexpr uint32_t kTwinMinLanes = 65536;
 constexpr int kStreamBlock = 256;    // threads per stream workgroup
 constexpr int kEncPer = 4;           // encode: 12-byte groups per thread per tile
 constexpr int kDecGpl = 8;           // decode: 4-unit groups per thread per tile
@@ -140,6 +146,11 @@ struct ShaWait {
 };
 constexpr uint32_t kShaWaitSlot = 8;  // done[g] = queue[kShaWaitSlot + g] (kShaQueueBytes)
 constexpr uint32_t kShaWaitMaxGroups = 48;
+// VGPRs per lane of the decode-ahead kernel pair (hipFuncGetAttributes): the
+// host sizes the two grids so that both are resident at once (the SHA waves
+// wait on every decode workgroup).
+int sha_wait_vgprs();
+int dec_ahead_vgprs();
 struct DecAhead {
     const uint64_t* gtile;  // group g = tiles [gtile[g], gtile[g + 1])
     uint32_t ngroups, grid;

@@ -226,32 +226,25 @@ __device__ __forceinline__ void plain_range(uint32_t (&st)[8], const Msg& m, uin
 }
 
 // Full blocks [kb, ke) of m into st and, from the same loads and schedule,
-// into the twin state s2 (kShaTwin).  Same pair fetch; unrolled x2 with a
-// register copy (a twin step is ~2,290 ops, so the copy costs < 1 %, and the
-// loop stays ~30 KB of code beside plain_range's ~45 KB).
+// into the twin state s2 (kShaTwin).  One block in flight while one is
+// compressed (two buffers): a twin step is ~2,290 ops (~4 us), long enough to
+// cover the load, and two buffers instead of plain_range's four keep the
+// kernel at a VGPR count that leaves room for the Base64 / decode waves.
 __device__ __forceinline__ void twin_range(uint32_t (&st)[8], uint32_t (&s2)[8], const Msg& m, uint32_t kb,
                                            uint32_t ke) {
-    uint32_t A[16], B[16], C[16], D[16], xa, xb, xc, xd;
+    uint32_t A[16], B[16], xa, xb;
     const uint32_t last = ke - 1u;
     load_block(m.p + 16u * kb, m.sh, A, xa);
-    load_block(m.p + 16u * min(kb + 1u, last), m.sh, B, xb);
     uint32_t k = kb;
     for (;;) {
-        load_block(m.p + 16u * min(k + 2u, last), m.sh, C, xc);
-        load_block(m.p + 16u * min(k + 3u, last), m.sh, D, xd);
+        load_block(m.p + 16u * min(k + 1u, last), m.sh, B, xb);
         to_be(A, xa, m.sel);
         compress2(st, s2, A);
         if (++k >= ke) break;
+        load_block(m.p + 16u * min(k + 1u, last), m.sh, A, xa);
         to_be(B, xb, m.sel);
         compress2(st, s2, B);
         if (++k >= ke) break;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            A[i] = C[i];
-            B[i] = D[i];
-        }
-        xa = xc;
-        xb = xd;
     }
 }
 
@@ -845,6 +838,11 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
 #undef DFS_SHA_ARGS
 
 }  // namespace
+
+int sha_wait_vgprs() {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(sha256_lanes_wait)) == hipSuccess ? a.numRegs : -1;
+}
 
 hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split,
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,

@@ -3,8 +3,8 @@ fragment that starts on the 64-byte block grid of its file's fileId lane rides
 in that lane — one load and one message schedule per block for both digests.
 That is fragment 0 of every file (SN:153, offset 0) and every fragment when the
 fragment size is a multiple of 64 (BASELINE configs[2]: 256 KiB, N = 8).
-Twins are built only for launches above dfs::kChainMaxLanes (32,768) lanes,
-so every batch here is larger than that.  Bit-exact against the oracle
+Twins are built only for launches that keep at least dfs::kTwinMinLanes
+(65,536) lanes, one wave per SIMD, so every batch here has that many.  Bit-exact against the oracle
 (fileId SN:127, fragment digests SN:159, Base64 SN:636) and, on download,
 decode + fragment verify + fileId verify (SN:281-282, 448-458).
 """
@@ -46,7 +46,7 @@ def _check_upload(engine, files, nfrag):
 # fragment 0 only (N = 5, 200-byte fragments start at 200, 400, ...: off the
 # grid); every fragment exactly one block; fragment 0 one block + 1 byte (the
 # others start off the grid).
-SHAPES = [(36000, 2048, 8), (40000, 1000, 5), (34000, 320, 5), (34000, 324, 5)]
+SHAPES = [(66000, 2048, 8), (40000, 1000, 5), (66000, 320, 5), (34000, 324, 5)]
 
 
 @pytest.mark.parametrize("nfiles,size,nfrag", SHAPES)
@@ -61,7 +61,7 @@ def test_twin_upload_ragged(engine):
     tail), random sizes, < 64-byte fragments (no twin) and empty files."""
     rng = np.random.default_rng(5)
     n = 36000
-    sizes = rng.integers(0, 6000, n)
+    sizes = rng.integers(0, 6000, n)  # 36,000 fileId lanes + the fragments that are not twins
     sizes[0::5] = 256 * rng.integers(1, 24, len(sizes[0::5]))
     sizes[1::5] = 256 * rng.integers(1, 24, len(sizes[1::5])) + rng.integers(1, 4, len(sizes[1::5]))
     sizes[2::97] = rng.integers(0, 256, len(sizes[2::97]))
@@ -70,7 +70,7 @@ def test_twin_upload_ragged(engine):
 
 
 @pytest.mark.parametrize("mode", ["overlap", "pipelined", "serial"])
-@pytest.mark.parametrize("nfiles,size,nfrag", [(36000, 2048, 8), (40000, 1000, 5)])
+@pytest.mark.parametrize("nfiles,size,nfrag", [(66000, 2048, 8), (40000, 1000, 5)])
 def test_twin_download(engine, mode, nfiles, size, nfrag, monkeypatch):
     """Download of twin-shaped batches: overlap (one SHA launch beside the
     fragment-ordered decode; twins inside the fileId lane's wait segments),
