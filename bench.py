@@ -144,6 +144,16 @@ def _free_port() -> int:
     return p
 
 
+_RESULT_OUT = None
+
+
+def emit(obj) -> None:
+    """The run's one JSON line, on the original stdout (see main)."""
+    out = _RESULT_OUT or sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
 def relaunch(args) -> int:
     """--gpus N > 1 without a launcher: start N ranks (one per GPU) with
     torch.distributed.run as a child process.  Runs before this process
@@ -600,7 +610,7 @@ def long_leg(args):
                             "achieved": round(b64_bytes / (k["b64_ms"] / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                             "unit": "GB/s"},
            "wall_ms_incl_synth": round(wall * 1e3, 3), "verified": bool(ok)}
-    print(json.dumps(res), flush=True)
+    emit(res)
     eng.close()
     return 0 if ok else 3
 
@@ -849,6 +859,14 @@ def main():
         args.mode = "serial"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return relaunch(args)
+    # Exactly one JSON line on stdout: native libraries write to fd 1 too
+    # (RCCL prints its version banner at communicator init), so fd 1 becomes
+    # stderr for the rest of the run and the result line goes to the original
+    # stdout.
+    global _RESULT_OUT
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -873,11 +891,11 @@ def main():
             dist.init_process_group("gloo", rank=0, world_size=1)
         per, ok, nbytes = dry_run(args, world, rank, log)
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-                              "warmup": args.warmup, "ms_per_step": round(per * 1e3, 3), "higher_is_better": True,
-                              "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "dry-run",
-                              "dry_run": True, "placed_bytes": nbytes, "verified": ok,
-                              "config": {"workload": "harness check (gloo, CPU tensors), no GPU work"}}), flush=True)
+            emit({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+                  "warmup": args.warmup, "ms_per_step": round(per * 1e3, 3), "higher_is_better": True,
+                  "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "dry-run",
+                  "dry_run": True, "placed_bytes": nbytes, "verified": ok,
+                  "config": {"workload": "harness check (gloo, CPU tensors), no GPU work"}})
         dist.destroy_process_group()
         return 0 if ok else 3
 
@@ -909,7 +927,7 @@ def main():
         elapsed = res["step_s"]
         value = F * S * world / elapsed / 1e9 if elapsed == elapsed else None
         if rank == 0:
-            print(json.dumps({
+            emit({
                 "metric": METRIC, "value": round(value, 3) if value else None, "unit": "GB/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(elapsed * 1e3, 3) if value else None, "higher_is_better": True,
@@ -921,7 +939,7 @@ def main():
                            "files_per_gpu": F, "file_bytes": S, "nfrag": N, "parallelism": f"files sharded x{world}",
                            "placement": args.placement},
                 "roofline": roofline_n(res, S, N) if ok else None,
-                "placement": res["placement"], "verified": ok}), flush=True)
+                "placement": res["placement"], "verified": ok})
         dist.destroy_process_group()
         return 0 if ok and not failures else 3
 
@@ -1084,7 +1102,7 @@ def main():
             failures.append("batcher")
     if failures:
         result["failed_legs"] = failures
-    print(json.dumps(result), flush=True)
+    emit(result)
     if args.no_batcher:
         plan.close()
     eng.close()

@@ -29,11 +29,14 @@ mkdir -p gpurun_out/prof_dl
 echo "== download kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dl/trace -o trace --output-format csv -- \
   python3 bench.py $DLARGS > gpurun_out/prof_dl/bench.json 2> gpurun_out/prof_dl/bench.err || fatal $?
+# PMC collection serializes dispatches: the decode-ahead SHA kernel would wait
+# out its bound for a decode that cannot run beside it, so the counter passes
+# run the download decode-then-SHA (DFS_DOWNLOAD_MODE=serial, same kernels).
 i=0
 for ctr in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   echo "== download pmc pass $i: $ctr"
-  timeout -s KILL 300 rocprofv3 --pmc $ctr -d gpurun_out/prof_dl/p$i -o pmc --output-format csv -- \
+  DFS_DOWNLOAD_MODE=serial timeout -s KILL 300 rocprofv3 --pmc $ctr -d gpurun_out/prof_dl/p$i -o pmc --output-format csv -- \
     python3 bench.py $DLARGS > gpurun_out/prof_dl/p$i.json 2> gpurun_out/prof_dl/p$i.err || fatal $?
 done
 python3 tools/pmc_summary.py gpurun_out/prof_dl gpurun_out/pmc_download_summary.json "${WORKLOAD_TAG:-65536x1048576/N5} download"

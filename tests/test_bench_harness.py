@@ -18,6 +18,9 @@ def _run(args, timeout=240):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
                        timeout=timeout, env=env, cwd=ROOT)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    # stdout holds the result line and nothing else (the driver parses it;
+    # library banners such as RCCL's go to stderr, bench.py main)
+    assert len(p.stdout.splitlines()) == len(lines), p.stdout[-2000:]
     return p.returncode, lines, p.stderr
 
 
