@@ -12,6 +12,6 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 cat gpurun_out/smoke.log
 [ -n "$NO_BENCH" ] && exit 0
 echo "== bench"
-timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
 cat gpurun_out/bench.json; tail -8 gpurun_out/bench.err
 exit $rc
