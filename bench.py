@@ -101,7 +101,9 @@ def parse(argv=None):
     ap.add_argument("--verify", type=int, default=8, help="files spot-checked against the oracle (rank 0)")
     ap.add_argument("--placement", choices=("star", "ring"), default="star",
                     help="N>1: placement inside the timed step (the other one is timed beside it)")
-    ap.add_argument("--chunks", type=int, default=4, help="N>1: file chunks pipelined through compute + placement")
+    ap.add_argument("--chunks", type=int, default=2,
+                    help="N>1: file chunks pipelined through compute + placement (2: 65,536-file launches keep the "
+                         "SHA twin lanes; chunk c of step k+1 waits only for chunk c's placement of step k)")
     ap.add_argument("--placement-step", action="store_true",
                     help="run the N>1 step (upload + RCCL placement, degraded read) at N=1 too: a one-rank "
                          "communicator, every node on this GPU (checks that code path on a one-GPU box)")
