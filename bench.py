@@ -327,21 +327,44 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
     reassemble_device(eng, addr, flen, F, N, out.data_ptr(), file_off, exp)
     torch.cuda.synchronize(dev)
     eng.set_profiling(True)
-    gat = []
+    gat, rtot = [], []
     for _ in range(reps):
         st, _dig = reassemble_device(eng, addr, flen, F, N, out.data_ptr(), file_off, exp)
-        gat.append(eng.timings()["gather"])
+        t = eng.timings()
+        gat.append(t["gather"]); rtot.append(t["total"])
         ok = ok and bool((st == 0).all())
     eng.set_profiling(False)
     ok = ok and bool(torch.equal(out, files[:F * S]))
+    # the same reassembly gather-then-SHA (serial ctx): the gather kernel's
+    # standalone rate and the serial time beside the default's
+    os.environ["DFS_DOWNLOAD_MODE"] = "serial"
+    try:
+        eng_s = dfs_amd.FragmentEngine(eng.device)
+    finally:
+        del os.environ["DFS_DOWNLOAD_MODE"]
+    s_gat, s_rtot = [], []
+    try:
+        out.zero_()
+        reassemble_device(eng_s, addr, flen, F, N, out.data_ptr(), file_off, exp)
+        eng_s.set_profiling(True)
+        for _ in range(reps):
+            st, _dig = reassemble_device(eng_s, addr, flen, F, N, out.data_ptr(), file_off, exp)
+            t = eng_s.timings()
+            s_gat.append(t["gather"]); s_rtot.append(t["total"])
+            ok = ok and bool((st == 0).all())
+    finally:
+        eng_s.close()
+    ok = ok and bool(torch.equal(out, files[:F * S]))
+    redo = eng.stats()["ovl_redo"]
     del out
-    gat_ms = float(np.mean(gat))
+    gat_ms = float(np.mean(s_gat))  # standalone gather (serial ctx)
     gat_gbs = 2 * F * S / (gat_ms / 1e3) / 1e9
     dev_ms = float(np.mean(tot))
     dec_ms = float(np.mean(s_dec))  # standalone decode (serial ctx)
     dec_bytes = int(msp[:, 1].sum()) + F * S  # Base64 read + bytes written
     log(f"download: {F} files, device {dev_ms:.1f} ms (decode span {np.mean(dec):.1f}, sha span {np.mean(sha):.1f}); "
-        f"serial {np.mean(s_tot):.1f} ms (decode {dec_ms:.1f}, sha {np.mean(s_sha):.1f}); raw gather {gat_ms:.1f} ms, "
+        f"serial {np.mean(s_tot):.1f} ms (decode {dec_ms:.1f}, sha {np.mean(s_sha):.1f}); raw reassembly + verify "
+        f"{np.mean(rtot):.1f} ms (serial {np.mean(s_rtot):.1f}, gather {gat_ms:.1f}), "
         f"ok={ok}, redo={redo}")
     if not ok:
         raise LegError("download leg: status or bytes differ")
@@ -357,10 +380,13 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
             "decode_ms": round(dec_ms, 3), "decode_gbs": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
             "decode_frac_hbm": round(dec_bytes / (dec_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "sha_ms": round(float(np.mean(s_sha)), 3),
+            "reassemble_ms": round(float(np.mean(rtot)), 3), "reassemble_serial_ms": round(float(np.mean(s_rtot)), 3),
             "gather_ms": round(gat_ms, 3), "gather_gbs": round(gat_gbs, 1),
             "gather_frac_hbm": round(gat_gbs / HBM_PEAK_GBS, 4), "ok": ok, "ovl_redo": redo,
             "note": "wall_ms includes host-side job planning per call; gbps = file bytes / device time; decode_* "
-                    "and sha_ms are the standalone kernels of the serial run"}
+                    "and sha_ms are the standalone kernels of the serial run; reassemble = the reference's raw-fragment "
+                    "download (SN:419-458: ordered gather + fileId verify), gather fragment by fragment beside the "
+                    "fileId SHA-256 (serial: gather, then SHA)"}
 
 
 def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):

@@ -403,7 +403,7 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out,
                              int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t prio, uint32_t wgs_per_cu,
-                             const DecAhead* ahead) {
+                             const StreamAhead* ahead) {
     if (ahead) {  // every workgroup takes part in every group (gdone counts workgroups)
         hipLaunchKernelGGL(b64_decode_kernel<true>, dim3(ahead->grid), dim3(kStreamBlock), 0, s, in, jobs, njobs, ntiles,
                            out, status, out_len, prio, ahead->gtile, ahead->ngroups, ahead->gdone);

@@ -72,6 +72,7 @@ struct dfs_ctx {
     int ovl_sha_wps = 3;         // overlap: SHA waves per SIMD (DFS_OVL_SHA_WPS) ...
     uint32_t ovl_dec_wgs = 1;    // ... and decode workgroups per CU beside them (DFS_OVL_DEC_WGS); both
                                  // clamped at open so the two grids are resident together (ovl_fit)
+    uint32_t ovl_gather_wgs = 2; // gather workgroups per CU beside them (reassembly overlap; fitted too)
     int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     uint32_t b64_prio = 3;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO)
     uint32_t dec_prio = 1;       // decode waves at s_setprio 3 beside SHA (DFS_DEC_PRIO=0: 0)
@@ -364,14 +365,20 @@ const char* dfs_strerror(int code) {
 // (one ~25 KB decode workgroup per wave slot) and the 32 waves per CU are far
 // from their limits.  Fewer decode workgroups first, then fewer SHA waves.
 static void ovl_fit(dfs_ctx* c) {
-    const int sv = dfs::sha_wait_vgprs(), dv = dfs::dec_ahead_vgprs();
-    if (sv <= 0 || dv <= 0) return;  // attributes unavailable: keep the defaults
-    const int sa = (sv + 7) / 8 * 8, da = (dv + 7) / 8 * 8;
+    const int sv = dfs::sha_wait_vgprs(), dv = dfs::dec_ahead_vgprs(), gv = dfs::gather_ahead_vgprs();
+    if (sv <= 0 || dv <= 0 || gv <= 0) {  // attributes unavailable: the smallest grids
+        c->ovl_sha_wps = 1;
+        c->ovl_dec_wgs = c->ovl_gather_wgs = 1;
+        return;
+    }
+    const int sa = (sv + 7) / 8 * 8, da = (dv + 7) / 8 * 8, ga = (gv + 7) / 8 * 8;
     while (c->ovl_sha_wps * sa + static_cast<int>(c->ovl_dec_wgs) * da > 512) {
         if (c->ovl_dec_wgs > 1) --c->ovl_dec_wgs;
         else if (c->ovl_sha_wps > 1) --c->ovl_sha_wps;
         else break;
     }
+    while (c->ovl_gather_wgs > 1 && c->ovl_sha_wps * sa + static_cast<int>(c->ovl_gather_wgs) * ga > 512)
+        --c->ovl_gather_wgs;
 }
 
 int dfs_open(dfs_ctx** out, int device) {
@@ -1120,48 +1127,138 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     } else {
         for (uint64_t k = 0; k < nf; ++k) src_addr[k] = reinterpret_cast<uint64_t>(src[k]);
     }
-    std::vector<StreamJob> jobs;
-    std::vector<uint64_t> items;
+    // Large batches whose fragments have the split lengths (the normal case)
+    // overlap the gather with the fileId SHA-256 as the download does: the
+    // gather runs fragment by fragment (group g = fragment g of every file),
+    // group 0 alone at full width, groups 1.. beside one SHA launch whose
+    // lanes wait for each group (ShaWait with nf = 0: every lane a fileId).
+    uint64_t nok = 0;
+    bool split_lens = true;
+    std::vector<uint64_t> soff(nfrag), slen(nfrag);
+    for (uint32_t f = 0; f < nfiles && split_lens; ++f) {
+        if (status[f] != DFS_OK) continue;
+        ++nok;
+        split(flen[f], nfrag, soff.data(), slen.data());
+        for (uint32_t i = 0; i < nfrag; ++i) split_lens = split_lens && frag_len[static_cast<uint64_t>(f) * nfrag + i] == slen[i];
+    }
+    const bool ovl = c->download_mode == 2 && split_lens && nfrag > 1 && nfrag <= dfs::kShaWaitMaxGroups &&
+                     nok > dfs::kChainMaxLanes;
+    std::vector<StreamJob> jobs, gj;
+    std::vector<uint64_t> items, gitems, gtile;
     std::vector<ShaDesc> sha;
+    std::vector<uint64_t> frag_dst(nf, 0);
     for (uint32_t f = 0; f < nfiles; ++f) {
         if (status[f] != DFS_OK) continue;
         uint64_t o = file_off[f];
         for (uint32_t i = 0; i < nfrag; ++i) {
             const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
-            if (frag_len[k]) {
-                StreamJob j{};
-                j.src_off = src_addr[k];
-                j.len = frag_len[k];
-                j.dst_off = o;  // ordered append, SN:448
-                j.id = static_cast<uint32_t>(k);
-                jobs.push_back(j);
-                items.push_back(copy_items(frag_len[k], reinterpret_cast<uintptr_t>(d_out + o)));
-            }
+            frag_dst[k] = o;  // ordered append, SN:448
             o += frag_len[k];
         }
         sha.push_back(msg(file_off[f], flen[f], f));  // SN:454
     }
-    const uint32_t njobs = static_cast<uint32_t>(jobs.size());
-    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(dfs::kGatherPer) * dfs::kStreamBlock);
+    // Jobs: file-major (serial), or fragment-major with group 0 in its own
+    // table and groups 1.. in a second one with continuous tile numbers.
+    uint64_t ntiles = 0, job2 = 0;
+    const uint64_t per = static_cast<uint64_t>(dfs::kGatherPer) * dfs::kStreamBlock;
+    auto add_job = [&](std::vector<StreamJob>& v, std::vector<uint64_t>& it, uint64_t k) {
+        if (!frag_len[k]) return;
+        StreamJob j{};
+        j.src_off = src_addr[k];
+        j.len = frag_len[k];
+        j.dst_off = frag_dst[k];
+        j.id = static_cast<uint32_t>(k);
+        v.push_back(j);
+        it.push_back(copy_items(frag_len[k], reinterpret_cast<uintptr_t>(d_out + frag_dst[k])));
+    };
+    if (!ovl) {
+        for (uint32_t f = 0; f < nfiles; ++f)
+            if (status[f] == DFS_OK)
+                for (uint32_t i = 0; i < nfrag; ++i) add_job(jobs, items, static_cast<uint64_t>(f) * nfrag + i);
+        ntiles = finish_jobs(jobs, items, per);
+    } else {
+        for (uint32_t f = 0; f < nfiles; ++f)
+            if (status[f] == DFS_OK) add_job(jobs, items, static_cast<uint64_t>(f) * nfrag);
+        ntiles = finish_jobs(jobs, items, per);
+        job2 = jobs.size();
+        uint64_t t = 0;
+        for (uint32_t i = 1; i < nfrag; ++i) {
+            gj.clear();
+            gitems.clear();
+            for (uint32_t f = 0; f < nfiles; ++f)
+                if (status[f] == DFS_OK) add_job(gj, gitems, static_cast<uint64_t>(f) * nfrag + i);
+            gtile.push_back(t);
+            const uint64_t gt = finish_jobs(gj, gitems, per);
+            for (size_t q = 0; q + 1 < gj.size(); ++q) {  // without the group's sentinel
+                gj[q].tile_start += t;
+                jobs.push_back(gj[q]);
+            }
+            t += gt;
+        }
+        gtile.push_back(t);
+        StreamJob sent{};
+        sent.tile_start = t;
+        jobs.push_back(sent);
+    }
+    const uint32_t njobs = static_cast<uint32_t>(ovl ? job2 - 1 : jobs.size() - 1);
     const uint32_t prio = sort_lanes(sha);
     if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
+    if (ovl)
+        if (int rc = put(c, B_JOBS2, gtile.data(), gtile.size() * sizeof(uint64_t), s)) return rc;
     HIPC(c->buf[B_DIG0].ensure(32ull * nfiles));
-    uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
-    tm.begin(DFS_T_TOTAL, s);
-    tm.begin(DFS_T_GATHER, s);
-    HIPC(dfs::launch_gather(c->buf[B_JOBS].as<StreamJob>(), njobs, ntiles, d_out, s));
-    tm.end(DFS_T_GATHER, s);
-    tm.begin(DFS_T_SHA, s);
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
-    HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
-                            d_dig, d_dig, c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s));
-    tm.end(DFS_T_SHA, s);
+    uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
+    uint32_t* d_queue = c->buf[B_QUEUE].as<uint32_t>();
+    const StreamJob* d_jobs = c->buf[B_JOBS].as<StreamJob>();
+    tm.begin(DFS_T_TOTAL, s);
+    if (!ovl) {
+        tm.begin(DFS_T_GATHER, s);
+        HIPC(dfs::launch_gather(d_jobs, njobs, ntiles, d_out, s));
+        tm.end(DFS_T_GATHER, s);
+        tm.begin(DFS_T_SHA, s);
+        HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
+                                d_dig, d_dig, d_queue, c->sha_wps, s));
+        tm.end(DFS_T_SHA, s);
+    } else {
+        if (!c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        if (c->pass_ev.empty()) {
+            hipEvent_t ev = nullptr;
+            HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            c->pass_ev.push_back(ev);
+        }
+        HIPC(hipMemsetAsync(d_queue, 0, dfs::kShaQueueBytes, s));  // the group counters (see dfs_download_batch)
+        tm.begin(DFS_T_GATHER, s);
+        HIPC(dfs::launch_gather(d_jobs, njobs, ntiles, d_out, s));
+        HIPC(hipEventRecord(c->pass_ev[0], s));
+        dfs::StreamAhead ah{c->buf[B_JOBS2].as<uint64_t>(), nfrag - 1, 256u * c->ovl_gather_wgs,
+                            d_queue + dfs::kShaWaitSlot + 1};
+        HIPC(dfs::launch_gather(d_jobs + job2, static_cast<uint32_t>(jobs.size() - job2 - 1), gtile.back(), d_out, s,
+                                &ah));
+        tm.end(DFS_T_GATHER, s);
+        HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[0], 0));
+        tm.begin(DFS_T_SHA, c->aux);
+        const dfs::ShaWait wt{d_queue + dfs::kShaWaitSlot, ah.grid, 1u, nfrag, 0u};
+        HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
+                                d_dig, d_dig, d_queue, c->ovl_sha_wps, c->aux, nullptr, nullptr, &wt));
+        tm.end(DFS_T_SHA, c->aux);
+        HIPC(hipEventRecord(c->join, c->aux));
+        HIPC(hipStreamWaitEvent(s, c->join, 0));
+    }
     tm.end(DFS_T_TOTAL, s);
     std::vector<uint8_t> dig(32ull * nfiles);
+    uint32_t timed_out = 0;
+    if (ovl) HIPC(hipMemcpyAsync(&timed_out, d_queue + 2, 4, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
     if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+    if (timed_out) {  // an in-kernel wait gave up: hash again now that the gather is complete
+        ++c->ovl_redo;
+        HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
+                                d_dig, d_dig, d_queue, c->sha_wps, s));
+        HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
     int rc = DFS_OK;
     for (uint32_t f = 0; f < nfiles; ++f) {
         if (status[f] == DFS_OK && expected && std::memcmp(dig.data() + 32ull * f, expected + 32ull * f, 32) != 0)
@@ -1349,7 +1446,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         tm.begin(DFS_T_B64DEC, s);
         HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(job0[1]), tiles[0], d_out, d_st, nullptr, s));
         HIPC(hipEventRecord(c->pass_ev[0], s));
-        dfs::DecAhead ah{c->buf[B_JOBS2].as<uint64_t>(), npass - 1, 256u * c->ovl_dec_wgs,
+        dfs::StreamAhead ah{c->buf[B_JOBS2].as<uint64_t>(), npass - 1, 256u * c->ovl_dec_wgs,
                          d_queue + dfs::kShaWaitSlot + 1};
         HIPC(dfs::launch_b64_decode(d_in, d_jobs + job2, static_cast<uint32_t>(jobs.size() - job2), gtile.back(), d_out,
                                     d_st, nullptr, s, c->dec_prio, 0, &ah));

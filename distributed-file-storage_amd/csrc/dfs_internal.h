@@ -146,12 +146,17 @@ struct ShaWait {
 };
 constexpr uint32_t kShaWaitSlot = 8;  // done[g] = queue[kShaWaitSlot + g] (kShaQueueBytes)
 constexpr uint32_t kShaWaitMaxGroups = 48;
-// VGPRs per lane of the decode-ahead kernel pair (hipFuncGetAttributes): the
-// host sizes the two grids so that both are resident at once (the SHA waves
-// wait on every decode workgroup).
+// VGPRs per lane of the kernels that run in "ahead" mode beside the waiting
+// SHA kernel (hipFuncGetAttributes): the host sizes the grids so that both
+// are resident at once (the SHA waves wait on every stream workgroup).
 int sha_wait_vgprs();
 int dec_ahead_vgprs();
-struct DecAhead {
+int gather_ahead_vgprs();
+// A stream kernel (decode, gather) in ahead mode: groups in order, every
+// workgroup takes its share of group g's tiles, publishes it (agent-scope
+// release) and adds 1 to gdone[g]; `grid` workgroups, all of them in every
+// group.
+struct StreamAhead {
     const uint64_t* gtile;  // group g = tiles [gtile[g], gtile[g + 1])
     uint32_t ngroups, grid;
     uint32_t* gdone;
@@ -179,7 +184,7 @@ hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_
 // grid = ahead->grid workgroups); the tile count is then ahead->gtile's.
 hipError_t launch_b64_decode(const char* in, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,
                              uint8_t* out, int32_t* status, uint64_t* out_len, hipStream_t s, uint32_t prio = 0,
-                             uint32_t wgs_per_cu = 8, const DecAhead* ahead = nullptr);
+                             uint32_t wgs_per_cu = 8, const StreamAhead* ahead = nullptr);
 // Framing bytes of n storeFragments bodies (digests: raw 32 B per file).
 hipError_t launch_store_body_frame(const StoreBody* bodies, uint32_t n, const uint8_t* digests, char* out,
                                    hipStream_t s);
@@ -189,7 +194,9 @@ hipError_t launch_store_body_parse(const char* in, const uint64_t* spans, uint32
                                    char* file_ids, hipStream_t s);
 // Gather: job.src_off is an absolute device address of the fragment; tiles
 // of kGatherPer x 256 16-byte chunks.
-hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s);
+// ahead: ahead mode (as launch_b64_decode).
+hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s,
+                         const StreamAhead* ahead = nullptr);
 hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
                         hipStream_t s, uint64_t file_off);
 

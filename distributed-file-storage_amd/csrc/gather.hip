@@ -22,10 +22,9 @@ typedef uint32_t g32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int P = kGatherPer;  // 16-byte chunks per thread per tile
 
-__global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* __restrict__ jobs, uint32_t njobs,
-                                                              uint64_t ntiles, uint8_t* __restrict__ out) {
-    uint64_t t0, t1;
-    tile_range(ntiles, t0, t1);
+// Tiles [t0, t1) of the job table.
+__device__ __forceinline__ void gather_range(const StreamJob* __restrict__ jobs, uint32_t njobs,
+                                             uint8_t* __restrict__ out, uint64_t t0, uint64_t t1) {
     if (t0 >= t1) return;
     uint32_t j = find_job(jobs, njobs, t0);
     for (uint64_t t = t0; t < t1; ++t) {
@@ -71,6 +70,29 @@ __global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* _
     }
 }
 
+// AHEAD (dfs_reassemble_verify, overlap mode): fragment groups in order, each
+// published to the SHA kernel beside it (StreamAhead, dfs_internal.h).
+template <bool AHEAD>
+__global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* __restrict__ jobs, uint32_t njobs,
+                                                              uint64_t ntiles, uint8_t* __restrict__ out,
+                                                              const uint64_t* __restrict__ gtile, uint32_t ngroups,
+                                                              uint32_t* __restrict__ gdone) {
+    if (!AHEAD) {
+        uint64_t t0, t1;
+        tile_range(ntiles, t0, t1);
+        gather_range(jobs, njobs, out, t0, t1);
+        return;
+    }
+    const uint64_t G = gridDim.x, b = blockIdx.x;
+    for (uint32_t g = 0; g < ngroups; ++g) {
+        const uint64_t a = gtile[g], n = gtile[g + 1] - a;
+        gather_range(jobs, njobs, out, a + n * b / G, a + n * (b + 1) / G);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(gdone + g, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -111,9 +133,21 @@ __global__ __launch_bounds__(kStreamBlock) void synth_kernel(uint8_t* __restrict
 
 }  // namespace
 
-hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s) {
+int gather_ahead_vgprs() {
+    hipFuncAttributes a{};
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(gather_kernel<true>)) == hipSuccess ? a.numRegs : -1;
+}
+
+hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s,
+                         const StreamAhead* ahead) {
+    if (ahead) {
+        hipLaunchKernelGGL(gather_kernel<true>, dim3(ahead->grid), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out,
+                           ahead->gtile, ahead->ngroups, ahead->gdone);
+        return hipGetLastError();
+    }
     if (ntiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_kernel, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles, out);
+    hipLaunchKernelGGL(gather_kernel<false>, dim3(stream_grid(ntiles)), dim3(kStreamBlock), 0, s, jobs, njobs, ntiles,
+                       out, nullptr, 0u, nullptr);
     return hipGetLastError();
 }
 

@@ -724,3 +724,50 @@ def test_download_pipelined_many_fragments_small_files(engine, mode, monkeypatch
     for f, (st, body) in enumerate(res):
         assert st == 0, (f, st)
         assert body == files[f], f
+
+
+@pytest.mark.parametrize("mode", ["overlap", "serial"])
+def test_reassemble_large_batch_overlap(engine, mode, monkeypatch):
+    """dfs_reassemble_verify above dfs::kChainMaxLanes files (SN:419-458, raw
+    fragments): default (overlap) gathers fragment 0 of every file first, then
+    the other fragments beside one fileId SHA-256 launch whose lanes wait for
+    each fragment group; serial: gather, then SHA.  Every file rebuilt and
+    verified against hashlib, plus a corrupted fragment ("File corrupted",
+    SN:455-458), a missing one (SN:443-446), empty and tiny files (fragments
+    of 0 bytes, several fragments starting inside one block), and a batch
+    whose fragment lengths are not the split's (a fetched fragment one byte
+    longer: the serial path, still verified)."""
+    if mode != "overlap":
+        monkeypatch.setenv("DFS_DOWNLOAD_MODE", mode)
+        engine = dfs_amd.FragmentEngine(0)
+    try:
+        rng = np.random.default_rng(91)
+        nfiles, nfrag = 34000, 5
+        sizes = rng.integers(0, 3000, nfiles)
+        sizes[:6] = [0, 1, 4, 5, 63, 64 * 5 + 3]
+        sizes[100] = sizes[200] = 1000
+        blob = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8).tobytes()
+        files, o = [], 0
+        for n in sizes:
+            files.append(blob[o:o + int(n)])
+            o += int(n)
+        frags = [[d[a:a + n] for a, n in O.c_split(len(d), nfrag)] for d in files]
+        ids = [hashlib.sha256(d).hexdigest() for d in files]
+        want = [0] * nfiles
+        frags[100][2] = bytes([frags[100][2][0] ^ 1]) + frags[100][2][1:]
+        want[100] = dfs_amd.DFS_E_CORRUPT
+        frags[200][3] = None
+        want[200] = dfs_amd.DFS_E_MISSING
+        res = engine.reassemble_verify(frags, ids)
+        assert engine.stats()["ovl_redo"] == 0
+        for f, (st, body, h) in enumerate(res):
+            assert st == want[f], (f, st, want[f])
+            if want[f] == 0:
+                assert body == files[f] and h == ids[f], f
+        frags2 = [list(x) for x in frags[:34000]]
+        frags2[7][1] = frags2[7][1] + b"\x00"  # not the split's length: whole batch serial
+        res2 = engine.reassemble_verify(frags2, ids)
+        assert res2[7][0] == dfs_amd.DFS_E_CORRUPT and res2[8][0] == 0 and res2[8][1] == files[8]
+    finally:
+        if mode != "overlap":
+            engine.close()
