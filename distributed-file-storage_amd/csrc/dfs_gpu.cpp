@@ -1382,11 +1382,15 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         // sort, so each 64-lane item waits for one group and the queue hands
         // out items in decode order.  File-major items would hold fragments
         // 1..N-1 of 16 files and wait for the last group.
-        if (ovl)
-            std::stable_sort(psha.begin(), psha.end(), [&](const ShaDesc& x, const ShaDesc& y) {
-                const uint32_t kx = x.out >= nf ? 0u : 1u + x.out % nfrag, ky = y.out >= nf ? 0u : 1u + y.out % nfrag;
-                return kx < ky;
-            });
+        if (ovl) {  // stable bucket pass by (fileId | fragment index), O(n)
+            auto key = [&](const ShaDesc& x) { return x.out >= nf ? 0u : 1u + static_cast<uint32_t>(x.out % nfrag); };
+            std::vector<size_t> start(nfrag + 2, 0);
+            for (const ShaDesc& x : psha) ++start[key(x) + 1];
+            for (uint32_t b = 0; b <= nfrag; ++b) start[b + 1] += start[b];
+            gfr.resize(psha.size());
+            for (const ShaDesc& x : psha) gfr[start[key(x)]++] = x;
+            psha.swap(gfr);
+        }
         prio[p] = sort_lanes(psha);  // one message per lane, longest first
         // Long items (balanced per SIMD, sha256_body): the fileId parts, which
         // are |group| fragments long; in a one-fragment pass every lane is
@@ -1423,6 +1427,7 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     if (ovl)
         if (int rc = put(c, B_JOBS2, gtile.data(), gtile.size() * sizeof(uint64_t), s)) return rc;
     HIPC(c->buf[B_STATUS].ensure(4ull * nf));
+    HIPC(c->buf[B_OUTLEN].ensure(4ull * nfiles));  // per-file verdicts (device-resident expected digests)
     HIPC(c->buf[B_DIG0].ensure(32ull * (nf + nfiles)));
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
     HIPC(hipMemsetAsync(c->buf[B_STATUS].p, 0, 4ull * nf, s));
@@ -1496,19 +1501,41 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         HIPC(hipStreamWaitEvent(s, c->join, 0));
     }
     tm.end(DFS_T_TOTAL, s);
-    std::vector<int32_t> st(nf);
-    std::vector<uint8_t> dig(32ull * (nf + nfiles));
+    // Expected digests already on the device (or none): the verdict is
+    // computed there and only one status word per file comes back.
+    const bool dev_verdict = dev && (!exp_frag || is_device_ptr(exp_frag)) && (!exp_file || is_device_ptr(exp_file));
+    std::vector<int32_t> st(dev_verdict ? nfiles : nf);
+    std::vector<uint8_t> dig(dev_verdict ? 0 : 32ull * (nf + nfiles));
+    auto fetch = [&]() -> int {
+        if (dev_verdict) {
+            HIPC(dfs::launch_download_verdict(d_st, d_dig, d_dig + 32ull * nf, exp_frag, exp_file, nfiles, nfrag,
+                                              c->buf[B_OUTLEN].as<int32_t>(), s));
+            HIPC(hipMemcpyAsync(st.data(), c->buf[B_OUTLEN].p, 4ull * nfiles, hipMemcpyDeviceToHost, s));
+        } else {
+            HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * nf, hipMemcpyDeviceToHost, s));
+            HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+        }
+        return DFS_OK;
+    };
     uint32_t timed_out = 0;
     if (ovl) HIPC(hipMemcpyAsync(&timed_out, d_queue + 2, 4, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * nf, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+    if (int e = fetch()) return e;
     if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     if (timed_out) {  // a decode-ahead wait gave up: hash again now that the decode is complete
         ++c->ovl_redo;
         HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
-        HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+        if (int e = fetch()) return e;
         HIPC(hipStreamSynchronize(s));
+    }
+    if (dev_verdict) {
+        int rc = DFS_OK;
+        for (uint32_t f = 0; f < nfiles; ++f) {
+            if (status[f] == DFS_OK && st[f])
+                status[f] = st[f] == 1 ? DFS_E_DECODE : (st[f] == 2 ? DFS_E_FRAG_MISMATCH : DFS_E_CORRUPT);
+            if (status[f] != DFS_OK && rc == DFS_OK) rc = status[f];
+        }
+        return rc;
     }
     std::vector<uint8_t> expf, expd;
     if (dev && exp_frag && is_device_ptr(exp_frag)) {  // expected digests may live on the device in device mode

@@ -197,6 +197,11 @@ hipError_t launch_store_body_parse(const char* in, const uint64_t* spans, uint32
 // ahead: ahead mode (as launch_b64_decode).
 hipError_t launch_gather(const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint8_t* out, hipStream_t s,
                          const StreamAhead* ahead = nullptr);
+// Download verdict per file on the device (expected digests in device
+// memory): verdict[f] = 0 good, 1 decode error, 2 fragment digest, 3 fileId.
+hipError_t launch_download_verdict(const int32_t* dec_status, const uint8_t* frag_dig, const uint8_t* file_dig,
+                                   const uint8_t* exp_frag, const uint8_t* exp_file, uint32_t nfiles, uint32_t nfrag,
+                                   int32_t* verdict, hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
                         hipStream_t s, uint64_t file_off);
 

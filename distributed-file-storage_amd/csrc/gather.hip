@@ -93,6 +93,33 @@ __global__ __launch_bounds__(kStreamBlock) void gather_kernel(const StreamJob* _
     }
 }
 
+// Per-file verdict of a download whose expected digests live on the device:
+// 1 = a fragment's Base64 was rejected (SN:281), 2 = a fragment digest differs
+// from the sender's (SN:250-257), 3 = the rebuilt file's digest differs from
+// its fileId (SN:454-458), 0 = good.  One thread per file; the host maps the
+// codes and keeps its own statuses (missing fragments) first.
+__global__ __launch_bounds__(256) void verdict_kernel(const int32_t* __restrict__ dec_status,
+                                                      const uint8_t* __restrict__ frag_dig,
+                                                      const uint8_t* __restrict__ file_dig,
+                                                      const uint8_t* __restrict__ exp_frag,
+                                                      const uint8_t* __restrict__ exp_file, uint32_t nfiles,
+                                                      uint32_t nfrag, int32_t* __restrict__ verdict) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nfiles) return;
+    int32_t v = 0;
+    for (uint32_t i = 0; i < nfrag && !v; ++i)
+        if (dec_status[static_cast<uint64_t>(f) * nfrag + i]) v = 1;
+    for (uint32_t i = 0; i < nfrag && !v && exp_frag; ++i) {
+        const uint64_t k = static_cast<uint64_t>(f) * nfrag + i;
+        for (uint32_t b = 0; b < 32; ++b)
+            if (frag_dig[32 * k + b] != exp_frag[32 * k + b]) v = 2;
+    }
+    if (!v && exp_file)
+        for (uint32_t b = 0; b < 32; ++b)
+            if (file_dig[32ull * f + b] != exp_file[32ull * f + b]) v = 3;
+    verdict[f] = v;
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -132,6 +159,15 @@ __global__ __launch_bounds__(kStreamBlock) void synth_kernel(uint8_t* __restrict
 }
 
 }  // namespace
+
+hipError_t launch_download_verdict(const int32_t* dec_status, const uint8_t* frag_dig, const uint8_t* file_dig,
+                                   const uint8_t* exp_frag, const uint8_t* exp_file, uint32_t nfiles, uint32_t nfrag,
+                                   int32_t* verdict, hipStream_t s) {
+    if (nfiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(verdict_kernel, dim3((nfiles + 255) / 256), dim3(256), 0, s, dec_status, frag_dig, file_dig,
+                       exp_frag, exp_file, nfiles, nfrag, verdict);
+    return hipGetLastError();
+}
 
 int gather_ahead_vgprs() {
     hipFuncAttributes a{};

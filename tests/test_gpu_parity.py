@@ -771,3 +771,55 @@ def test_reassemble_large_batch_overlap(engine, mode, monkeypatch):
     finally:
         if mode != "overlap":
             engine.close()
+
+
+@pytest.mark.parametrize("mode", ["overlap", "serial"])
+def test_device_download_verdicts(engine, mode, monkeypatch):
+    """dfs_download_batch on device buffers with the expected digests in HBM:
+    the per-file verdict is computed on the device (verdict_kernel) — a Base64
+    char outside the alphabet (SN:281 -> DFS_E_DECODE), a wrong expected
+    fragment digest (SN:250-257 -> DFS_E_FRAG_MISMATCH), a wrong fileId
+    (SN:454-458 -> DFS_E_CORRUPT), a fragment no holder had (SN:443-446 ->
+    DFS_E_MISSING) — and every other file rebuilt bit-exact.  6,000 files x 6
+    lanes: above kChainMaxLanes, so the overlap (default) or serial path."""
+    import torch
+    from dfs_amd import placement as P
+    from dfs_amd.engine import download_device
+    if mode != "overlap":
+        monkeypatch.setenv("DFS_DOWNLOAD_MODE", mode)
+        engine = dfs_amd.FragmentEngine(0)
+    try:
+        nfiles, S, nfrag = 6000, 3001, 5
+        spans = np.array([(f * S, S) for f in range(nfiles)], dtype=np.uint64)
+        files = torch.empty(nfiles * S + 8, dtype=torch.uint8, device="cuda")
+        dfs_amd.synth_fill(engine, files.data_ptr(), spans, 77, O.SYNTH_SEED)
+        plan = dfs_amd.UploadPlan(engine, spans, nfrag, frag_major=True)
+        fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
+        frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
+        b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+        plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
+        torch.cuda.synchronize()
+        msp = P.frag_major_spans([S] * nfiles, nfrag).copy()
+        want = np.zeros(nfiles, dtype=np.int32)
+        k = 7 * nfrag + 3
+        b64[int(msp[k, 0]) + 5] = ord("!")
+        want[7] = dfs_amd.DFS_E_DECODE
+        frd[(3 * nfrag + 2) * 32] ^= 1
+        want[3] = dfs_amd.DFS_E_FRAG_MISMATCH
+        fd[5 * 32 + 31] ^= 0x80
+        want[5] = dfs_amd.DFS_E_CORRUPT
+        msp[9 * nfrag + 4, 1] = np.uint64(dfs_amd.DFS_SPAN_MISSING)
+        want[9] = dfs_amd.DFS_E_MISSING
+        out = torch.zeros(nfiles * S, dtype=torch.uint8, device="cuda")
+        st = download_device(engine, b64.data_ptr(), msp, nfiles, nfrag, np.full(nfiles, S, np.uint64),
+                             frd.data_ptr(), fd.data_ptr(), out.data_ptr(),
+                             np.arange(nfiles, dtype=np.uint64) * np.uint64(S))
+        assert engine.stats()["ovl_redo"] == 0
+        assert st.tolist() == want.tolist()
+        good = np.nonzero(want == 0)[0]
+        o, f0 = out.view(nfiles, S), files[:nfiles * S].view(nfiles, S)
+        assert torch.equal(o[torch.as_tensor(good)], f0[torch.as_tensor(good)])
+        plan.close()
+    finally:
+        if mode != "overlap":
+            engine.close()
