@@ -528,10 +528,14 @@ def batcher_leg(args, log):
     """Thread-per-connection clients (SN:28-31), one 1 MiB file per request,
     through the library's batcher (dfs_submit_upload / dfs_submit_download,
     host buffers: PCIe in and out) at each concurrency in --clients, closed
-    loop for --client-seconds.  The clients are native threads
-    (tools/batcher_load, a child process); the fileIds it reports are checked
-    here.  Beside it the CPU proxy at the same concurrency (min(C, cores)
-    threads, one file per thread)."""
+    loop for --client-seconds, in two buffer modes: "staged" (pageable
+    handler buffers: each handler copies its bytes into and out of the
+    worker's pinned staging) and "pinned" (handler buffers from
+    dfs_host_alloc: the worker's DMA reads / writes them, no host copies).
+    The clients are native threads (tools/batcher_load, a child process); the
+    fileIds it reports are checked here.  Beside it the CPU proxy at the same
+    concurrency (min(C, cores) threads, one file per thread), upload and
+    download."""
     import hashlib
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # checker + cpu_baseline leg only
@@ -542,42 +546,60 @@ def batcher_leg(args, log):
     rows, ok, cpu_one = [], True, None
     for C in [int(x) for x in args.clients.split(",") if x]:
         row = {"clients": C}
-        for kind in ("upload", "download"):
-            p = subprocess.run([tool, str(C), str(args.client_seconds), kind, str(S), str(N), "500", "3"],
-                               capture_output=True, text=True, timeout=300)
-            if p.returncode != 0:
-                raise LegError(f"batcher_load {C} {kind}: rc {p.returncode}: {p.stderr[-300:]} {p.stdout[-300:]}")
-            r = json.loads(p.stdout.strip().splitlines()[-1])
-            ok &= r["ok"] and [r["file0_id"], r["file1_id"]] == want
-            row[kind] = {k: r[k] for k in ("requests", "gbps", "p50_ms", "p99_ms")}
-            st = r["stats"]
-            row[kind]["batches"] = st["batches"]
-            row[kind]["mean_batch"] = round(st["requests"] / max(st["batches"], 1), 1)
-            row[kind]["device_ms_per_batch"] = round(st["device_s"] / max(st["batches"], 1) * 1e3, 2)
+        for pinned in (0, 1):
+            for kind in ("upload", "download"):
+                p = subprocess.run([tool, str(C), str(args.client_seconds), kind, str(S), str(N), "2000", "3",
+                                    str(pinned)], capture_output=True, text=True, timeout=300)
+                if p.returncode != 0:
+                    raise LegError(f"batcher_load {C} {kind} pinned={pinned}: rc {p.returncode}: {p.stderr[-300:]} "
+                                   f"{p.stdout[-300:]}")
+                r = json.loads(p.stdout.strip().splitlines()[-1])
+                ok &= r["ok"] and [r["file0_id"], r["file1_id"]] == want
+                key = kind + ("_pinned" if pinned else "")
+                row[key] = {k: r[k] for k in ("requests", "gbps", "p50_ms", "p99_ms")}
+                st = r["stats"]
+                row[key]["batches"] = st["batches"]
+                row[key]["direct"] = st["direct"]
+                row[key]["mean_batch"] = round(st["requests"] / max(st["batches"], 1), 1)
+                row[key]["device_ms_per_batch"] = round(st["device_s"] / max(st["batches"], 1) * 1e3, 2)
+                row[key]["client_cpu_us_per_req"] = round(r["client_cpu_us_per_req"]["in_submit"], 1)
+                row[key]["cgroup_throttled_s"] = r["throttled_s"]
         th_cpu = min(C, cores)
         nf = max(th_cpu, int(th_cpu / 0.0012))  # ~1 s of work
         secs, _, _ = O.cpu_upload_bench(nf, S, N, th_cpu, use_openssl=True)
         cpu = nf * S / secs / 1e9 if secs > 0 else None
         if C == 1 and secs > 0:
             cpu_one = secs / nf
+        nd = max(th_cpu, int(th_cpu / 0.0012))
+        dsecs = O.cpu_download_bench(nd, S, N, th_cpu, True)
         row["cpu_upload_gbps"] = round(cpu, 3) if cpu else None
+        row["cpu_download_gbps"] = round(nd * S / dsecs / 1e9, 3) if dsecs > 0 else None
         row["cpu_threads"] = th_cpu
         if cpu_one:  # one handler's file, queued behind C / threads others
             row["cpu_latency_est_ms"] = round(cpu_one * 1e3 * ((C + th_cpu - 1) // th_cpu), 2)
         rows.append(row)
-        log(f"batcher: {C} clients: upload {row['upload']['gbps']} GB/s p50 {row['upload']['p50_ms']} ms "
-            f"(batch {row['upload']['mean_batch']}, device {row['upload']['device_ms_per_batch']} ms), "
-            f"download {row['download']['gbps']} GB/s p50 {row['download']['p50_ms']} ms; cpu {row['cpu_upload_gbps']}")
-    cross = next((r["clients"] for r in rows if r["cpu_upload_gbps"] and r["upload"]["gbps"] > r["cpu_upload_gbps"]),
-                 None)
+        log(f"batcher: {C} clients: upload {row['upload']['gbps']} / pinned {row['upload_pinned']['gbps']} GB/s "
+            f"p50 {row['upload_pinned']['p50_ms']} ms (batch {row['upload_pinned']['mean_batch']}), download "
+            f"{row['download']['gbps']} / pinned {row['download_pinned']['gbps']} GB/s; cpu {row['cpu_upload_gbps']} / "
+            f"{row['cpu_download_gbps']}")
+
+    def cross(key, cpu_key):
+        return next((r["clients"] for r in rows if r[cpu_key] and r[key]["gbps"] > r[cpu_key]), None)
     if not ok:
         raise LegError("batcher leg: a client result is wrong")
-    return {"file_bytes": S, "nfrag": N, "rows": rows, "crossover_clients_upload": cross, "ok": ok,
-            "cpu_cores": cores,
-            "note": "native client threads (tools/batcher_load), host buffers: each request crosses PCIe in and "
-                    "out; latency = one handler's blocking call; cpu = the oracle's C proxy with min(C, cores) "
-                    "threads (OpenSSL SHA-256 + scalar Base64); cpu_latency_est = one file's single-thread time x "
-                    "ceil(C / threads)"}
+    return {"file_bytes": S, "nfrag": N, "rows": rows,
+            "crossover_clients": {"upload": cross("upload", "cpu_upload_gbps"),
+                                  "download": cross("download", "cpu_download_gbps"),
+                                  "upload_pinned": cross("upload_pinned", "cpu_upload_gbps"),
+                                  "download_pinned": cross("download_pinned", "cpu_download_gbps")},
+            "ok": ok, "cpu_cores": cores,
+            "note": "native client threads (tools/batcher_load, 3 workers, 2 ms window), host buffers: each request "
+                    "crosses PCIe in and out; staged = pageable handler buffers copied by the handler into / out of "
+                    "pinned staging, pinned = dfs_host_alloc buffers moved by DMA directly (direct = such requests); "
+                    "latency = one handler's blocking call; cpu = the oracle's C proxy with min(C, cores) threads "
+                    "(OpenSSL SHA-256 + scalar Base64, upload and download sequences); cpu_latency_est = one file's "
+                    "single-thread time x ceil(C / threads); crossover = fewest clients where the GPU path beats the "
+                    "CPU proxy"}
 
 
 def long_leg(args):

@@ -28,14 +28,17 @@
 // Whoever publishes a phase notifies while holding that lock, so the other
 // side cannot see the phase, finish and free the object first.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <thread>
 #include <vector>
 
@@ -47,6 +50,23 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
+
+// dfs_host_alloc buffers (base -> bytes): a request is direct only if each
+// of its buffers lies inside one of them, so the DMA never touches pageable
+// memory.
+std::shared_mutex g_pin_mu;
+std::map<uintptr_t, uint64_t> g_pinned;
+
+bool in_pinned(const void* p, uint64_t n) {
+    if (!n) return true;
+    if (!p) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::shared_lock<std::shared_mutex> lk(g_pin_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return a - it->first <= it->second && n <= it->second - (a - it->first);
+}
 
 struct Req;
 
@@ -88,6 +108,7 @@ struct Req {
     uint8_t* in_dst = nullptr;         // staging slot of the input
     const uint8_t* out_src = nullptr;  // staging of the output
     int status = DFS_OK;
+    bool direct = false;  // input and output in dfs_host_alloc buffers: DMA'd by the worker, no staging
     std::mutex mu;  // guards phase (and the fields the phase publishes)
     std::condition_variable cv;
 };
@@ -128,7 +149,7 @@ struct Buf {
 struct Worker {
     dfs_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;  // blocking-sync event: the worker sleeps instead of spinning on the CPU share
+    hipEvent_t done = nullptr;  // polled with sleeps (dfs::quiet_wait): the worker does not spin on the CPU share
     Buf pin_in, pin_out, d_in, d_out, d_dig;
     std::thread th;
     Worker() {
@@ -154,7 +175,8 @@ struct dfs_batcher {
 namespace {
 
 bool wait_stream(Worker& w) {
-    return hipEventRecord(w.done, w.stream) == hipSuccess && hipEventSynchronize(w.done) == hipSuccess;
+    // not hipEventSynchronize: it spins a core for the whole batch (dfs::quiet_wait)
+    return hipEventRecord(w.done, w.stream) == hipSuccess && dfs::quiet_wait(w.done) == hipSuccess;
 }
 
 struct Timing {
@@ -163,44 +185,58 @@ struct Timing {
 
 double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
 
-// Give every request its staging slot and wait until all copied their input.
-void stage_in(dfs_batcher* B, std::vector<Req*>& batch, BatchSync& bs, uint8_t* base,
+// Give the first `staged` requests their staging slots and wait until they
+// copied their input (direct requests have nothing to copy).
+void stage_in(dfs_batcher* B, std::vector<Req*>& batch, size_t staged, BatchSync& bs, uint8_t* base,
               const std::vector<uint64_t>& off, Timing& tm) {
     const auto t0 = Clock::now();
-    for (size_t i = 0; i < batch.size(); ++i) {
+    for (size_t i = 0; i < staged; ++i) {
         batch[i]->in_dst = base + off[i];
         publish(batch[i], 1);
     }
     std::unique_lock<std::mutex> lk(bs.mu);
-    bs.cv.wait(lk, [&] { return bs.copied_in == batch.size(); });
+    bs.cv.wait(lk, [&] { return bs.copied_in == staged; });
     tm.stage_in = since(t0);
+}
+
+// Staged requests first (their bytes form one contiguous prefix of the
+// staging and device buffers: one DMA each way), direct ones after.
+size_t order_batch(std::vector<Req*>& batch) {
+    auto mid = std::stable_partition(batch.begin(), batch.end(), [](const Req* r) { return !r->direct; });
+    return static_cast<size_t>(mid - batch.begin());
 }
 
 int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs, Timing& tm) {
     const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
+    const size_t staged = order_batch(batch);
     std::vector<dfs_span> spans(n);
     std::vector<uint64_t> in_off(n);
-    uint64_t total = 0, b64_total = 0;
+    uint64_t total = 0, b64_total = 0, staged_in = 0, staged_b64 = 0;
     for (uint32_t i = 0; i < n; ++i) {
         in_off[i] = total;
         spans[i] = dfs_span{total, batch[i]->len};
         total += (batch[i]->len + 15) & ~15ull;  // 16-byte aligned file starts
         b64_total += batch[i]->b64_off[N];       // filled at submit: the request's Base64 bytes
+        if (i + 1 == staged) staged_in = total, staged_b64 = b64_total;
     }
     const uint64_t dig_bytes = 32ull * n * (N + 1);
-    int rc = w.pin_in.grow(total + 16);
-    if (!rc) rc = w.pin_out.grow(dig_bytes + b64_total + 16);
+    int rc = w.pin_in.grow(staged_in + 16);
+    if (!rc) rc = w.pin_out.grow(dig_bytes + staged_b64 + 16);
     if (!rc) rc = w.d_in.grow(total + 16);
     if (!rc) rc = w.d_out.grow(b64_total + 16);
     if (!rc) rc = w.d_dig.grow(dig_bytes);
     if (rc) return rc;
-    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off, tm);
+    stage_in(B, batch, staged, bs, w.pin_in.as<uint8_t>(), in_off, tm);
     const auto t_dev = Clock::now();
     std::vector<uint64_t> b64_off(static_cast<uint64_t>(n) * N + 1);
     uint8_t* d_fd = w.d_dig.as<uint8_t>();
     uint8_t* d_frd = d_fd + 32ull * n;
-    if (total && hipMemcpyAsync(w.d_in.p, w.pin_in.p, total, hipMemcpyHostToDevice, w.stream) != hipSuccess)
+    if (staged_in && hipMemcpyAsync(w.d_in.p, w.pin_in.p, staged_in, hipMemcpyHostToDevice, w.stream) != hipSuccess)
         return DFS_E_HIP;
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i)  // direct: from the handler's pinned buffer
+        if (batch[i]->len && hipMemcpyAsync(w.d_in.as<uint8_t>() + in_off[i], batch[i]->file, batch[i]->len,
+                                            hipMemcpyHostToDevice, w.stream) != hipSuccess)
+            return DFS_E_HIP;
     // one stream per worker (DFS_SERIAL: the Base64 kernel follows the SHA
     // kernel on it): a box exposes few hardware queues (GPU_MAX_HW_QUEUES=4),
     // and streams sharing one would serialise the workers' batches
@@ -209,21 +245,30 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
     if (rc) return rc;
     uint8_t* h = w.pin_out.as<uint8_t>();
     if (hipMemcpyAsync(h, d_fd, dig_bytes, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
-        (b64_total && hipMemcpyAsync(h + dig_bytes, w.d_out.p, b64_total, hipMemcpyDeviceToHost, w.stream) != hipSuccess) ||
-        !wait_stream(w))
+        (staged_b64 && hipMemcpyAsync(h + dig_bytes, w.d_out.p, staged_b64, hipMemcpyDeviceToHost, w.stream) != hipSuccess))
         return DFS_E_HIP;
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i) {  // direct: into the handler's pinned buffer
+        const Req* r = batch[i];
+        if (r->out_bytes && hipMemcpyAsync(r->b64, w.d_out.as<char>() + b64_off[static_cast<uint64_t>(i) * N],
+                                           r->out_bytes, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
+            return DFS_E_HIP;
+    }
+    if (!wait_stream(w)) return DFS_E_HIP;
     tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
         Req* r = batch[i];
         std::memcpy(r->fd, h + 32ull * i, 32);
         std::memcpy(r->frd, h + 32ull * n + 32ull * N * i, 32ull * N);
-        r->out_src = h + dig_bytes + b64_off[static_cast<uint64_t>(i) * N];  // its Base64, [fragment] order
+        // its Base64, [fragment] order (direct: already in place)
+        r->out_src = i < staged ? h + dig_bytes + b64_off[static_cast<uint64_t>(i) * N] : nullptr;
     }
     return DFS_OK;
 }
 
 int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs, Timing& tm) {
     const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
+    const size_t staged = order_batch(batch);
+    uint64_t staged_in = 0, staged_out = 0;
     const bool have_f = batch.front()->exp_frag != nullptr, have_i = batch.front()->exp_file != nullptr;
     std::vector<uint64_t> in_off(n), file_len(n), file_off(n);
     std::vector<dfs_span> spans(static_cast<uint64_t>(n) * N);
@@ -247,36 +292,64 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
         file_len[i] = r->len;
         file_off[i] = out_total;
         out_total += (r->len + 15) & ~15ull;
+        if (i + 1 == staged) staged_in = total, staged_out = out_total;
         if (have_f) std::memcpy(ef.data() + 32ull * N * i, r->exp_frag, 32ull * N);
         if (have_i) std::memcpy(ei.data() + 32ull * i, r->exp_file, 32);
     }
-    int rc = w.pin_in.grow(total + 16);
-    if (!rc) rc = w.pin_out.grow(out_total + 16);
+    int rc = w.pin_in.grow(staged_in + 16);
+    if (!rc) rc = w.pin_out.grow(staged_out + 16);
     if (!rc) rc = w.d_in.grow(total + 16);
     if (!rc) rc = w.d_out.grow(out_total + 16);
     if (rc) return rc;
-    stage_in(B, batch, bs, w.pin_in.as<uint8_t>(), in_off, tm);
+    stage_in(B, batch, staged, bs, w.pin_in.as<uint8_t>(), in_off, tm);
     const auto t_dev = Clock::now();
-    if (total && hipMemcpyAsync(w.d_in.p, w.pin_in.p, total, hipMemcpyHostToDevice, w.stream) != hipSuccess)
+    if (staged_in && hipMemcpyAsync(w.d_in.p, w.pin_in.p, staged_in, hipMemcpyHostToDevice, w.stream) != hipSuccess)
         return DFS_E_HIP;
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i) {  // direct: the fragments' Base64, packed
+        const Req* r = batch[i];
+        uint8_t* d = w.d_in.as<uint8_t>() + in_off[i];
+        const char* run = nullptr;  // fragments back to back in the handler's buffer go as one DMA
+        uint64_t run_len = 0;
+        for (uint32_t k = 0; k <= N; ++k) {
+            const bool end = k == N;
+            const dfs_span sp = end ? dfs_span{0, 0} : r->frags[k];
+            if (!end && (sp.len == DFS_SPAN_MISSING || !sp.len)) continue;
+            if (!end && run && r->text + sp.off == run + run_len) {
+                run_len += sp.len;
+                continue;
+            }
+            if (run_len) {
+                if (hipMemcpyAsync(d, run, run_len, hipMemcpyHostToDevice, w.stream) != hipSuccess) return DFS_E_HIP;
+                d += run_len;
+            }
+            run = end ? nullptr : r->text + sp.off;
+            run_len = end ? 0 : sp.len;
+        }
+    }
     std::vector<int32_t> st(n);
     rc = dfs_download_batch(w.ctx, w.d_in.as<char>(), spans.data(), n, N, file_len.data(), have_f ? ef.data() : nullptr,
                             have_i ? ei.data() : nullptr, w.d_out.as<uint8_t>(), file_off.data(), st.data(),
                             DFS_DEVICE_PTRS);
     if (rc != DFS_OK && rc != DFS_E_MISSING && rc != DFS_E_DECODE && rc != DFS_E_FRAG_MISMATCH && rc != DFS_E_CORRUPT)
         return rc;
-    if (out_total && (hipMemcpyAsync(w.pin_out.p, w.d_out.p, out_total, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
-                      !wait_stream(w)))
+    if (staged_out && hipMemcpyAsync(w.pin_out.p, w.d_out.p, staged_out, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
         return DFS_E_HIP;
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i)  // direct, good files only (as the staged copy-out)
+        if (st[i] == DFS_OK && batch[i]->len &&
+            hipMemcpyAsync(batch[i]->out, w.d_out.as<uint8_t>() + file_off[i], batch[i]->len, hipMemcpyDeviceToHost,
+                           w.stream) != hipSuccess)
+            return DFS_E_HIP;
+    if (!wait_stream(w)) return DFS_E_HIP;
     tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
         batch[i]->status = st[i];
-        batch[i]->out_src = w.pin_out.as<uint8_t>() + file_off[i];
+        batch[i]->out_src = i < staged ? w.pin_out.as<uint8_t>() + file_off[i] : nullptr;
     }
     return DFS_OK;
 }
 
 void worker_main(dfs_batcher* B, Worker* w) {
+    (void)pthread_setname_np(pthread_self(), "dfs-batch");  // per-thread CPU accounting (tools/batcher_load)
     (void)hipSetDevice(B->device);
     const auto window = std::chrono::microseconds(B->o.max_wait_us);
     for (;;) {
@@ -309,6 +382,7 @@ void worker_main(dfs_batcher* B, Worker* w) {
             ++B->st.batches;
             B->st.requests += batch.size();
             B->st.max_batch = std::max<uint64_t>(B->st.max_batch, batch.size());
+            for (const Req* r : batch) B->st.direct += r->direct;
             for (Req* r : batch) B->st.queue_s += std::chrono::duration<double>(now - r->arrive).count();
             if (!B->q.empty()) B->cv_work.notify_one();
         }
@@ -414,7 +488,7 @@ int dfs_batcher_create(int device, uint32_t nfrag, const dfs_batcher_opts* opts,
         B->workers.push_back(w);
         rc = dfs_open(&w->ctx, device);
         if (rc == DFS_OK) w->stream = dfs::ctx_stream(w->ctx);  // the ctx's own stream: one hardware queue per worker
-        if (rc == DFS_OK && hipEventCreateWithFlags(&w->done, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess)
+        if (rc == DFS_OK && hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess)
             rc = DFS_E_HIP;
     }
     if (rc == DFS_OK)
@@ -446,6 +520,31 @@ int dfs_batcher_destroy(dfs_batcher* B) {
     return DFS_OK;
 }
 
+int dfs_host_alloc(uint64_t bytes, void** p) {
+    if (!p) return DFS_E_ARG;
+    *p = nullptr;
+    void* q = nullptr;
+    if (hipHostMalloc(&q, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return DFS_E_NOMEM;
+    }
+    std::unique_lock<std::shared_mutex> lk(g_pin_mu);
+    g_pinned[reinterpret_cast<uintptr_t>(q)] = bytes;
+    *p = q;
+    return DFS_OK;
+}
+
+int dfs_host_free(void* p) {
+    if (!p) return DFS_E_ARG;
+    {
+        std::unique_lock<std::shared_mutex> lk(g_pin_mu);
+        auto it = g_pinned.find(reinterpret_cast<uintptr_t>(p));
+        if (it == g_pinned.end()) return DFS_E_ARG;
+        g_pinned.erase(it);
+    }
+    return hipHostFree(p) == hipSuccess ? DFS_OK : DFS_E_HIP;
+}
+
 int dfs_batcher_stats(dfs_batcher* B, dfs_batcher_stats_t* out) {
     if (!B || !out) return DFS_E_ARG;
     std::lock_guard<std::mutex> lk(B->mu);
@@ -471,6 +570,7 @@ int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t
     r.frd = frag_digest;
     r.b64 = b64;
     r.b64_off = b64_off;
+    r.direct = in_pinned(file, len) && in_pinned(b64, r.out_bytes);
     return submit(B, r);
 }
 
@@ -491,6 +591,9 @@ int dfs_submit_download(dfs_batcher* B, const char* b64, const dfs_span* frags, 
     r.exp_frag = expected_frag_digest;
     r.exp_file = expected_file_digest;
     r.out = out;
+    r.direct = in_pinned(out, file_len);
+    for (uint32_t k = 0; k < B->nfrag && r.direct; ++k)
+        if (frags[k].len != DFS_SPAN_MISSING) r.direct = in_pinned(b64 + frags[k].off, frags[k].len);
     return submit(B, r);
 }
 

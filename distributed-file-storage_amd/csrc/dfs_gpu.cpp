@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <functional>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +20,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dfs_gpu.h"
@@ -87,6 +89,7 @@ struct dfs_ctx {
     // dfs_set_stream) first waits for scratch_ev (recorded after the last
     // launch that used them) so it cannot overwrite descriptors in flight.
     hipEvent_t scratch_ev = nullptr;
+    hipEvent_t sync_ev = nullptr;  // quiet_sync (calls run under mu, so one per ctx)
     hipStream_t scratch_stream = nullptr;
     // Pinned staging for the host -> device descriptor copies of one call
     // (two arenas, alternating per call): an async copy from pageable memory
@@ -108,6 +111,40 @@ struct dfs_ctx {
 
 namespace dfs {
 hipStream_t ctx_stream(dfs_ctx* c) { return c->stream(); }
+
+// hipStreamSynchronize / hipEventSynchronize busy-wait on this runtime, even
+// for hipEventBlockingSync events: a 29 ms wait costs 29 ms of host CPU
+// (tools/host_probe, profiles/r02c_host_probe.txt).  StorageNode runs one
+// thread per connection (SN:30), and a handler blocked in a call must not
+// spend a core of the node's share on nothing, so the synchronous calls poll
+// an event with sleeps growing from 8 to 256 us (at most ~0.25 ms late on a
+// call that runs milliseconds; 0.35 ms of CPU per 29 ms wait).
+hipError_t quiet_wait(hipEvent_t ev) {
+    unsigned us = 8;
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) {
+            (void)hipGetLastError();  // the not-ready answers are not errors of this thread
+            return e;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+        if (us < 256) us *= 2;
+    }
+}
+
+hipError_t quiet_sync(dfs_ctx* c, hipStream_t s) {
+    const hipError_t e = hipEventRecord(c->sync_ev, s);
+    return e == hipSuccess ? quiet_wait(c->sync_ev) : e;
+}
+
+// Device -> host copy into caller (usually pageable) memory.  Such a copy
+// returns only when done and, issued behind running kernels, spins a core
+// until they finish; so the stream is drained quietly first.
+hipError_t d2h(dfs_ctx* c, void* dst, const void* src, size_t n, hipStream_t s) {
+    hipError_t e = quiet_sync(c, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s);
+    return e;
+}
 int ctx_device(dfs_ctx* c) { return c->device; }
 std::mutex& ctx_store_mutex(dfs_ctx* c) { return c->store_mu; }
 StoreStaging*& ctx_store(dfs_ctx* c) { return c->store; }
@@ -283,7 +320,7 @@ struct Scratch {
         if (c->scratch_stream && c->scratch_stream != s) (void)hipStreamWaitEvent(s, c->scratch_ev, 0);
         c->cur_arena ^= 1;
         auto& a = c->arena[c->cur_arena];
-        if (a.pending) (void)hipEventSynchronize(a.ev);
+        if (a.pending) (void)dfs::quiet_wait(a.ev);
         a.pending = false;
         a.used = 0;
     }
@@ -302,7 +339,7 @@ int put(dfs_ctx* c, int id, const void* src, size_t n, hipStream_t s) {
     auto& a = c->arena[c->cur_arena];
     if (n <= kArenaMax) {
         if (a.used + n > a.cap) {
-            if (a.used) HIPC(hipStreamSynchronize(s));  // this call's earlier copies still read the arena
+            if (a.used) HIPC(dfs::quiet_sync(c, s));  // this call's earlier copies still read the arena
             const size_t want = std::max<size_t>({a.used + n, 2 * a.cap, size_t(1) << 20});
             if (a.p) (void)hipHostFree(a.p);
             a.p = nullptr;
@@ -410,6 +447,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming);
     for (auto& a : c->arena)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&a.ev, hipEventDisableTiming);
     if (e != hipSuccess) {
@@ -429,7 +467,7 @@ int dfs_close(dfs_ctx* c) {
     dfs::store_staging_free(c->store);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : {c->fork, c->join, c->scratch_ev})
+    for (hipEvent_t ev : {c->fork, c->join, c->scratch_ev, c->sync_ev})
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : c->pass_ev) (void)hipEventDestroy(ev);
     for (auto& a : c->arena) {
@@ -463,7 +501,7 @@ int dfs_get_timings(dfs_ctx* c, float* ms, int n) {
     for (int k = 0; k < n && k < DFS_T_COUNT; ++k) {
         ms[k] = -1.0f;
         if (!c->ev_used[k]) continue;
-        HIPC(hipEventSynchronize(c->ev[2 * k + 1]));
+        HIPC(dfs::quiet_wait(c->ev[2 * k + 1]));
         HIPC(hipEventElapsedTime(&ms[k], c->ev[2 * k], c->ev[2 * k + 1]));
     }
     return DFS_OK;
@@ -533,8 +571,8 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
-        HIPC(hipMemcpyAsync(digests, d_dig, 32ull * n, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        HIPC(dfs::d2h(c, digests, d_dig, 32ull * n, s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     return DFS_OK;
 }
@@ -583,9 +621,9 @@ int dfs_sha256_update_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* par
     tm.end(DFS_T_SHA, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
-        if (fin) HIPC(hipMemcpyAsync(digests, d_dig, 32ull * n, hipMemcpyDeviceToHost, s));
-        else HIPC(hipMemcpyAsync(state, d_state, 32ull * n, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        if (fin) HIPC(dfs::d2h(c, digests, d_dig, 32ull * n, s));
+        else HIPC(dfs::d2h(c, state, d_state, 32ull * n, s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     return DFS_OK;
 }
@@ -623,8 +661,8 @@ int dfs_receive_fragments_batch(dfs_ctx* c, const char* in, const dfs_span* msgs
         HIPC(dfs::launch_sha256(out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(d.size()),
                                 static_cast<uint32_t>(d.size()), prio, c->buf[B_DIG1].as<uint8_t>(),
                                 c->buf[B_DIG1].as<uint8_t>(), c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s));
-        HIPC(hipMemcpyAsync(dig.data(), c->buf[B_DIG1].p, dig.size(), hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        HIPC(dfs::d2h(c, dig.data(), c->buf[B_DIG1].p, dig.size(), s));
+        HIPC(dfs::quiet_sync(c, s));
     } else {
         if (int e = dfs_sha256_batch(c, out, ok.data(), static_cast<uint32_t>(ok.size()), dig.data(), 0)) return e;
     }
@@ -714,8 +752,8 @@ int dfs_b64_encode_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, 
     tm.end(DFS_T_B64ENC, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
-        if (total) HIPC(hipMemcpyAsync(out, d_out, total, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        if (total) HIPC(dfs::d2h(c, out, d_out, total, s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     return DFS_OK;
 }
@@ -768,10 +806,10 @@ int dfs_b64_decode_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint3
     tm.end(DFS_T_B64DEC, s);
     tm.end(DFS_T_TOTAL, s);
     std::vector<int32_t> st(n);
-    HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * n, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(out_len, c->buf[B_OUTLEN].p, 8ull * n, hipMemcpyDeviceToHost, s));
-    if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
+    HIPC(dfs::d2h(c, st.data(), c->buf[B_STATUS].p, 4ull * n, s));
+    HIPC(dfs::d2h(c, out_len, c->buf[B_OUTLEN].p, 8ull * n, s));
+    if (!dev && out_end) HIPC(dfs::d2h(c, out, d_out, out_end, s));
+    HIPC(dfs::quiet_sync(c, s));
     int rc = DFS_OK;
     for (uint32_t i = 0; i < n; ++i) {
         status[i] = st[i] ? DFS_E_DECODE : DFS_OK;
@@ -1077,10 +1115,10 @@ int dfs_upload_batch(dfs_ctx* c, const uint8_t* files, const dfs_span* spans, ui
     if (int rc = scratch_plan(c, h, nfiles, nfrag, s, p)) return rc;
     if (int rc = run_plan_locked(c, &p, d_files, d_fd, d_frd, d_b64, flags)) return rc;
     if (!dev) {
-        if (!(flags & DFS_NO_FILEID)) HIPC(hipMemcpyAsync(fd, d_fd, 32ull * nfiles, hipMemcpyDeviceToHost, s));
-        HIPC(hipMemcpyAsync(frd, d_frd, 32ull * nf, hipMemcpyDeviceToHost, s));
-        if (do_b64 && h.total) HIPC(hipMemcpyAsync(b64, d_b64, h.total, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        if (!(flags & DFS_NO_FILEID)) HIPC(dfs::d2h(c, fd, d_fd, 32ull * nfiles, s));
+        HIPC(dfs::d2h(c, frd, d_frd, 32ull * nf, s));
+        if (do_b64 && h.total) HIPC(dfs::d2h(c, b64, d_b64, h.total, s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     return DFS_OK;
 }
@@ -1248,16 +1286,16 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
     tm.end(DFS_T_TOTAL, s);
     std::vector<uint8_t> dig(32ull * nfiles);
     uint32_t timed_out = 0;
-    if (ovl) HIPC(hipMemcpyAsync(&timed_out, d_queue + 2, 4, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
-    if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
+    if (ovl) HIPC(dfs::d2h(c, &timed_out, d_queue + 2, 4, s));
+    HIPC(dfs::d2h(c, dig.data(), d_dig, dig.size(), s));
+    if (!dev && out_end) HIPC(dfs::d2h(c, out, d_out, out_end, s));
+    HIPC(dfs::quiet_sync(c, s));
     if (timed_out) {  // an in-kernel wait gave up: hash again now that the gather is complete
         ++c->ovl_redo;
         HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
                                 d_dig, d_dig, d_queue, c->sha_wps, s));
-        HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        HIPC(dfs::d2h(c, dig.data(), d_dig, dig.size(), s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     int rc = DFS_OK;
     for (uint32_t f = 0; f < nfiles; ++f) {
@@ -1510,23 +1548,23 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         if (dev_verdict) {
             HIPC(dfs::launch_download_verdict(d_st, d_dig, d_dig + 32ull * nf, exp_frag, exp_file, nfiles, nfrag,
                                               c->buf[B_OUTLEN].as<int32_t>(), s));
-            HIPC(hipMemcpyAsync(st.data(), c->buf[B_OUTLEN].p, 4ull * nfiles, hipMemcpyDeviceToHost, s));
+            HIPC(dfs::d2h(c, st.data(), c->buf[B_OUTLEN].p, 4ull * nfiles, s));
         } else {
-            HIPC(hipMemcpyAsync(st.data(), c->buf[B_STATUS].p, 4ull * nf, hipMemcpyDeviceToHost, s));
-            HIPC(hipMemcpyAsync(dig.data(), d_dig, dig.size(), hipMemcpyDeviceToHost, s));
+            HIPC(dfs::d2h(c, st.data(), c->buf[B_STATUS].p, 4ull * nf, s));
+            HIPC(dfs::d2h(c, dig.data(), d_dig, dig.size(), s));
         }
         return DFS_OK;
     };
     uint32_t timed_out = 0;
-    if (ovl) HIPC(hipMemcpyAsync(&timed_out, d_queue + 2, 4, hipMemcpyDeviceToHost, s));
+    if (ovl) HIPC(dfs::d2h(c, &timed_out, d_queue + 2, 4, s));
     if (int e = fetch()) return e;
-    if (!dev && out_end) HIPC(hipMemcpyAsync(out, d_out, out_end, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
+    if (!dev && out_end) HIPC(dfs::d2h(c, out, d_out, out_end, s));
+    HIPC(dfs::quiet_sync(c, s));
     if (timed_out) {  // a decode-ahead wait gave up: hash again now that the decode is complete
         ++c->ovl_redo;
         HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
         if (int e = fetch()) return e;
-        HIPC(hipStreamSynchronize(s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     if (dev_verdict) {
         int rc = DFS_OK;
@@ -1595,7 +1633,7 @@ int dfs_synth_fill_at(dfs_ctx* c, uint8_t* d_dst, const dfs_span* files, uint32_
     const uint64_t ntiles = finish_jobs(jobs, items, dfs::kStreamBlock);
     if (int rc = put(c, B_JOBS2, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
     HIPC(dfs::launch_synth(d_dst, c->buf[B_JOBS2].as<StreamJob>(), njobs, ntiles, seed, s, file_off));
-    HIPC(hipStreamSynchronize(s));  // the job table lives in reusable scratch
+    HIPC(dfs::quiet_sync(c, s));  // the job table lives in reusable scratch
     return DFS_OK;
 }
 
@@ -1686,8 +1724,8 @@ int dfs_store_bodies_build(dfs_ctx* c, const uint8_t* files, const dfs_span* fil
     tm.end(DFS_T_B64ENC, s);
     tm.end(DFS_T_TOTAL, s);
     if (!dev) {
-        HIPC(hipMemcpyAsync(bodies, d_out, total, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        HIPC(dfs::d2h(c, bodies, d_out, total, s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     return DFS_OK;
 }
@@ -1726,9 +1764,9 @@ int dfs_store_bodies_receive(dfs_ctx* c, const char* bodies, const dfs_span* bod
         HIPC(c->buf[B_DIG1].ensure(64ull * n));
         HIPC(dfs::launch_store_body_parse(d_in, c->buf[B_JOBS].as<uint64_t>(), n, c->buf[B_DESC].as<dfs::BodyParse>(),
                                           c->buf[B_DIG1].as<char>(), s));
-        HIPC(hipMemcpyAsync(parsed.data(), c->buf[B_DESC].p, sizeof(dfs::BodyParse) * n, hipMemcpyDeviceToHost, s));
-        HIPC(hipMemcpyAsync(file_ids, c->buf[B_DIG1].p, 64ull * n, hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        HIPC(dfs::d2h(c, parsed.data(), c->buf[B_DESC].p, sizeof(dfs::BodyParse) * n, s));
+        HIPC(dfs::d2h(c, file_ids, c->buf[B_DIG1].p, 64ull * n, s));
+        HIPC(dfs::quiet_sync(c, s));
     }
     // Decode each payload into the body's output slot and hash it (SN:280-282).
     std::vector<dfs_span> msgs;

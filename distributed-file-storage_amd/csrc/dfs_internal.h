@@ -210,6 +210,10 @@ hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uin
 struct StoreStaging;
 void store_staging_free(StoreStaging* s);
 hipStream_t ctx_stream(dfs_ctx* c);
+// Wait for an event / for everything queued on a ctx stream without spinning
+// a host core (dfs_gpu.cpp).
+hipError_t quiet_wait(hipEvent_t ev);
+hipError_t quiet_sync(dfs_ctx* c, hipStream_t s);
 int ctx_device(dfs_ctx* c);
 std::mutex& ctx_store_mutex(dfs_ctx* c);  // guards the staging ring only
 StoreStaging*& ctx_store(dfs_ctx* c);

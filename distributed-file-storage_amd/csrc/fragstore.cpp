@@ -430,7 +430,7 @@ int dfs_store_write_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t
             pos += run;
             i = j;
         }
-        if (rc == DFS_OK && (hipEventRecord(stg->ev[k], s) != hipSuccess || hipEventSynchronize(stg->ev[k]) != hipSuccess))
+        if (rc == DFS_OK && (hipEventRecord(stg->ev[k], s) != hipSuccess || dfs::quiet_wait(stg->ev[k]) != hipSuccess))
             rc = DFS_E_HIP;
         if (rc != DFS_OK) break;
         slot_latch[k].add(static_cast<int>(batch.size()));
@@ -533,7 +533,7 @@ int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t*
     auto fill = [&](size_t b) -> int {
         const int k = static_cast<int>(b % kSlots);
         if (pending[k]) {
-            if (hipEventSynchronize(stg->ev[k]) != hipSuccess) return DFS_E_HIP;
+            if (dfs::quiet_wait(stg->ev[k]) != hipSuccess) return DFS_E_HIP;
             pending[k] = false;
         }
         slot_latch[k].add(static_cast<int>(batches[b].size()));
@@ -571,7 +571,8 @@ int dfs_store_read_fragments(dfs_ctx* ctx, const char* node_root, const uint8_t*
         if (rc == DFS_OK && b + ahead < batches.size()) rc = fill(b + ahead);
     }
     for (auto& l : slot_latch) l.wait();
-    if (hipStreamSynchronize(s) != hipSuccess && rc == DFS_OK) rc = DFS_E_HIP;
+    for (int k = 0; k < kSlots; ++k)  // the last copy out of every slot (recorded after it)
+        if (pending[k] && dfs::quiet_wait(stg->ev[k]) != hipSuccess && rc == DFS_OK) rc = DFS_E_HIP;
     return finish(c, status, rc);
 }
 

@@ -56,7 +56,8 @@ class dfs_span(ctypes.Structure):
 class dfs_batcher_stats_t(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("max_batch", ctypes.c_uint64),
                 ("queue_s", ctypes.c_double), ("stage_in_s", ctypes.c_double), ("device_s", ctypes.c_double),
-                ("stage_out_s", ctypes.c_double), ("enqueue_s", ctypes.c_double), ("return_s", ctypes.c_double)]
+                ("stage_out_s", ctypes.c_double), ("enqueue_s", ctypes.c_double), ("return_s", ctypes.c_double),
+                ("direct", ctypes.c_uint64)]
 
 
 class dfs_batcher_opts(ctypes.Structure):
@@ -113,6 +114,8 @@ SIGNATURES = {
     "dfs_batcher_create": (_int, [_int, _u32, _vp, ctypes.POINTER(_vp)]),
     "dfs_batcher_destroy": (_int, [_vp]),
     "dfs_batcher_stats": (_int, [_vp, _vp]),
+    "dfs_host_alloc": (_int, [_u64, ctypes.POINTER(_vp)]),
+    "dfs_host_free": (_int, [_vp]),
     "dfs_submit_upload": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
     "dfs_submit_download": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "dfs_comm_unique_id": (_int, [_vp]),

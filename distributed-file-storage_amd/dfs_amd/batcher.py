@@ -13,6 +13,30 @@ from . import _lib as L
 from ._lib import check, dfs_batcher_opts, lib
 
 
+class PinnedBuffer:
+    """A dfs_host_alloc buffer (page-locked host memory) viewed as a uint8
+    numpy array.  Requests whose buffers all lie in such buffers are "direct":
+    the batcher's DMA reads / writes them, no staging copy on the handler."""
+
+    def __init__(self, nbytes: int):
+        self._p = ctypes.c_void_p()
+        check(lib().dfs_host_alloc(nbytes, ctypes.byref(self._p)), "dfs_host_alloc")
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(self._p.value))[:nbytes]
+
+    def free(self) -> None:
+        if self._p:
+            self.array = None
+            check(lib().dfs_host_free(self._p), "dfs_host_free")
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Batcher:
     def __init__(self, device: int, nfrag: int, max_wait_us: int = 0, max_files: int = 0, max_bytes: int = 0,
                  depth: int = 0):
@@ -42,6 +66,15 @@ class Batcher:
         check(self.upload_into(a, fd, frd, b64, off), "dfs_submit_upload")
         return (fd.tobytes(), [frd[i].tobytes() for i in range(self.nfrag)],
                 [b64[int(off[i]):int(off[i + 1])].tobytes() for i in range(self.nfrag)])
+
+    def download_into(self, text: np.ndarray, spans, file_len: int, ef: Optional[np.ndarray],
+                      ei: Optional[np.ndarray], out: np.ndarray) -> int:
+        """handleDownload's pipeline for one file from / into caller buffers:
+        text (uint8 Base64 chars), spans (dfs_span * nfrag into text), out
+        (>= file_len bytes).  Returns the DFS status."""
+        return lib().dfs_submit_download(self._b, text.ctypes.data, spans, file_len,
+                                         ef.ctypes.data if ef is not None else None,
+                                         ei.ctypes.data if ei is not None else None, out.ctypes.data)
 
     def download(self, b64_frags: Sequence[Optional[bytes]], file_len: int, frag_digests: Optional[Sequence[bytes]],
                  file_digest: Optional[bytes]) -> Tuple[int, Optional[bytes]]:

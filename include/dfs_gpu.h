@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DFS_ABI_VERSION 2
+#define DFS_ABI_VERSION 3
 
 /* Return codes. */
 #define DFS_OK 0
@@ -348,8 +348,11 @@ int dfs_upload_plan_destroy(dfs_upload_plan* plan);
  * every request queued within max_wait_us of the oldest (or until max_files
  * / max_bytes) as one launch, and `depth` workers keep batches in flight
  * (each has its own ctx, stream, pinned staging and device buffers).  All
- * buffers are host memory; the caller's bytes are copied by its own thread
- * into / out of pinned staging.  Thread-safe; results are bit-identical to
+ * buffers are host memory.  A request whose input AND output each lie inside
+ * one dfs_host_alloc buffer is "direct": the worker's DMA reads and writes
+ * those buffers, nothing is copied on the host.  Any other request's bytes
+ * are copied by its own (handler) thread into / out of the worker's pinned
+ * staging.  Thread-safe; results are bit-identical to
  * dfs_upload_batch / dfs_download_batch on the same file.  Zero fields of
  * opts take the defaults (200 us, 1024 files, 1 GiB, depth 2). */
 typedef struct dfs_batcher dfs_batcher;
@@ -361,6 +364,13 @@ typedef struct dfs_batcher_opts {
     uint32_t reserved;
 } dfs_batcher_opts;
 int dfs_batcher_create(int device, uint32_t nfrag, const dfs_batcher_opts* opts, dfs_batcher** batcher);
+/* Pinned host memory for request buffers (a handler's upload body, its
+ * Base64 answer, the file it returns): page-locked, so the batcher moves a
+ * direct request over PCIe without a staging copy.  From Java: allocate the
+ * per-connection buffers once (MemorySegment.ofAddress(p).reinterpret(n)).
+ * dfs_host_free takes exactly the pointer dfs_host_alloc returned. */
+int dfs_host_alloc(uint64_t bytes, void** p);
+int dfs_host_free(void* p);
 /* Stops accepting requests, finishes the queued ones, joins the workers. */
 int dfs_batcher_destroy(dfs_batcher* batcher);
 typedef struct dfs_batcher_stats_t {
@@ -371,6 +381,7 @@ typedef struct dfs_batcher_stats_t {
     double stage_out_s;  /* workers waiting for handlers to copy outputs out     */
     double enqueue_s;    /* handlers' time from the call to holding a queue slot */
     double return_s;     /* handlers' time from results ready to returning       */
+    uint64_t direct;     /* requests moved straight from / to dfs_host_alloc buffers */
 } dfs_batcher_stats_t;
 int dfs_batcher_stats(dfs_batcher* batcher, dfs_batcher_stats_t* stats);
 /* One upload (SN:127, 138-159, 636): file_digest[32], frag_digest[nfrag*32],

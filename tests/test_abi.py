@@ -38,7 +38,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_strerror():
     L = dfs_amd.lib()
-    assert L.dfs_abi_version() == 2
+    assert L.dfs_abi_version() == 3
     assert L.dfs_strerror(dfs_amd.DFS_E_CORRUPT) == b"File corrupted"
     assert L.dfs_strerror(dfs_amd.DFS_E_MISSING) == b"Could not retrieve fragment"
 

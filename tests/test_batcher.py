@@ -104,3 +104,65 @@ def test_single_request_latency_path():
         efd, efrd, eb64, _ = O.c_upload_batch([data], 5)
         assert fd == efd[0].tobytes() and b"".join(texts) == eb64
         assert b.stats()["batches"] == 1
+
+
+def test_direct_pinned_requests_mixed_with_staged():
+    """Handlers whose buffers come from dfs_host_alloc (direct: the worker's
+    DMA reads / writes them) share batches with handlers on pageable memory
+    (staged); every result bit-exact vs the oracle, a failed download leaves
+    the caller's output untouched in both modes."""
+    from dfs_amd import _lib as L
+    from dfs_amd.batcher import PinnedBuffer
+    nfrag, threads, per = 5, 48, 3
+    with Batcher(0, nfrag, max_wait_us=3000) as b:
+        def work(t):
+            direct = t % 2 == 0
+            for k in range(per):
+                i = t * per + k
+                data = _file(i)
+                n = len(data)
+                efd, efrd, eb64, eoff = O.c_upload_batch([data], nfrag)
+                cap = len(eb64) + 16
+                if direct:
+                    fin, bout = PinnedBuffer(max(n, 1)), PinnedBuffer(cap)
+                    src, b64 = fin.array[:n], bout.array
+                else:
+                    src, b64 = np.frombuffer(data, np.uint8).copy(), np.zeros(cap, np.uint8)
+                if direct:
+                    src[:] = np.frombuffer(data, np.uint8)
+                fd, frd, off = np.zeros(32, np.uint8), np.zeros((nfrag, 32), np.uint8), np.zeros(nfrag + 1, np.uint64)
+                assert b.upload_into(src, fd, frd, b64, off) == 0, i
+                assert fd.tobytes() == efd[0].tobytes() and frd.tobytes() == efrd[0].tobytes(), i
+                assert b64[:int(off[nfrag])].tobytes() == eb64, i
+                # download from the same (pinned or pageable) Base64, into a
+                # (pinned or pageable) output; every third one corrupt
+                spans = (L.dfs_span * nfrag)()
+                for j in range(nfrag):
+                    spans[j].off, spans[j].len = int(off[j]), int(off[j + 1] - off[j])
+                bad = k == 2 and n > 0
+                ei = np.frombuffer(bytes(32) if bad else fd.tobytes(), np.uint8)
+                dout = PinnedBuffer(max(n, 1)) if direct else None
+                out = dout.array if direct else np.zeros(max(n, 1), np.uint8)
+                out[:] = 0xA5
+                st = b.download_into(b64, spans, n, frd.reshape(-1), ei, out)
+                if bad:
+                    assert st == dfs_amd.DFS_E_CORRUPT and (out == 0xA5).all(), (i, st)
+                else:
+                    assert st == 0 and out[:n].tobytes() == data, (i, st)
+                for pb in ([fin, bout, dout] if direct else []):
+                    pb.free()
+        _run_threads(threads, work)
+        s = b.stats()
+        assert s["requests"] == 2 * threads * per
+        assert s["direct"] == threads * per  # half the handlers, uploads and downloads
+        assert s["batches"] < s["requests"]
+
+
+def test_host_alloc_registry():
+    from dfs_amd import _lib as L
+    import ctypes
+    p = ctypes.c_void_p()
+    assert L.lib().dfs_host_alloc(4096, ctypes.byref(p)) == 0 and p.value
+    assert L.lib().dfs_host_free(ctypes.c_void_p(p.value + 8)) == dfs_amd.DFS_E_ARG  # not an allocation start
+    assert L.lib().dfs_host_free(p) == 0
+    assert L.lib().dfs_host_free(p) == dfs_amd.DFS_E_ARG  # already freed

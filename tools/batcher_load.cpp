@@ -7,16 +7,23 @@
 // carries no interpreter lock.  Prints one JSON line; bench.py runs it per
 // concurrency and checks the printed fileIds against its own checker.
 //
-//   batcher_load <clients> <seconds> <upload|download> <file_bytes> <nfrag> [max_wait_us] [depth]
+//   batcher_load <clients> <seconds> <upload|download> <file_bytes> <nfrag> [max_wait_us] [depth] [pinned]
+// pinned = 1: every client's buffers come from dfs_host_alloc (direct
+// requests: DMA straight from / into them, no staging copies).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <dirent.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "../include/dfs_gpu.h"
 
@@ -68,11 +75,52 @@ void cpu_stat(unsigned long long& usage, unsigned long long& throttled) {
     }
 }
 
+double thread_cpu_now() {
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+// CPU seconds (utime + stime) of this process's threads, split into the
+// client threads (tids), the batcher's workers (named "dfs-batch") and the
+// rest (main thread, HIP / ROCr runtime threads).
+void thread_cpu(const std::vector<long>& tids, double& clients, double& workers, double& other) {
+    clients = workers = other = 0;
+    const double hz = static_cast<double>(sysconf(_SC_CLK_TCK));
+    DIR* d = opendir("/proc/self/task");
+    if (!d) return;
+    while (dirent* e = readdir(d)) {
+        if (e->d_name[0] == '.') continue;
+        const long tid = std::atol(e->d_name);
+        char path[96], comm[64] = {0};
+        std::snprintf(path, sizeof path, "/proc/self/task/%ld/comm", tid);
+        if (FILE* f = std::fopen(path, "r")) {
+            if (!std::fgets(comm, sizeof comm, f)) comm[0] = 0;
+            std::fclose(f);
+        }
+        std::snprintf(path, sizeof path, "/proc/self/task/%ld/stat", tid);
+        FILE* f = std::fopen(path, "r");
+        if (!f) continue;
+        char buf[1024];
+        const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+        std::fclose(f);
+        buf[n] = 0;
+        const char* p = std::strrchr(buf, ')');  // fields after the comm: state is field 3, utime 14, stime 15
+        unsigned long long ut = 0, st = 0;
+        if (!p || std::sscanf(p + 2, "%*c %*d %*d %*d %*d %*d %*u %*u %*u %*u %*u %llu %llu", &ut, &st) != 2) continue;
+        const double s = (ut + st) / hz;
+        if (std::find(tids.begin(), tids.end(), tid) != tids.end()) clients += s;
+        else if (!std::strncmp(comm, "dfs-batch", 9)) workers += s;
+        else other += s;
+    }
+    closedir(d);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
     if (argc < 6) {
-        std::fprintf(stderr, "usage: %s clients seconds upload|download file_bytes nfrag [max_wait_us] [depth]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s clients seconds upload|download file_bytes nfrag [max_wait_us] [depth] [pinned]\n", argv[0]);
         return 2;
     }
     const int C = std::atoi(argv[1]);
@@ -83,6 +131,21 @@ int main(int argc, char** argv) {
     dfs_batcher_opts o{};
     if (argc > 6) o.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
     if (argc > 7) o.depth = static_cast<uint32_t>(std::atoi(argv[7]));
+    const bool pinned = argc > 8 && std::atoi(argv[8]) != 0;
+    // a client buffer: pageable (std::vector) or a dfs_host_alloc buffer
+    struct HostBuf {
+        std::vector<uint8_t> v;
+        void* p = nullptr;
+        uint8_t* data() { return p ? static_cast<uint8_t*>(p) : v.data(); }
+        void make(uint64_t n, bool pin) {
+            if (pin && dfs_host_alloc(n ? n : 1, &p) == DFS_OK) return;
+            p = nullptr;
+            v.assign(n ? n : 1, 0);
+        }
+        ~HostBuf() {
+            if (p) dfs_host_free(p);
+        }
+    };
     if (C < 1 || N < 1 || N > 64) return 2;
     dfs_batcher* B = nullptr;
     if (int rc = dfs_batcher_create(0, N, &o, &B)) {
@@ -104,18 +167,30 @@ int main(int argc, char** argv) {
             return 3;
         }
     }
+    std::vector<HostBuf> text(kDistinct);  // the Base64 download clients read (pinned if asked)
+    for (int f = 0; f < kDistinct; ++f) {
+        text[f].make(cap, pinned);
+        std::memcpy(text[f].data(), b64[f].data(), cap);
+    }
     std::atomic<int> ready{0};
     std::atomic<bool> go{false}, bad{false};
     std::atomic<int> first_rc{0}, mismatches{0};
     std::vector<std::vector<double>> lat(C);
+    std::vector<double> cpu_in(C, 0.0), cpu_out(C, 0.0);  // thread CPU inside / outside the submit calls (window)
     Clock::time_point deadline, measure_from;
     std::vector<std::thread> th;
+    std::vector<long> tids(C, 0);
     th.reserve(C);
     for (int t = 0; t < C; ++t) {
         th.emplace_back([&, t] {
             const int f = t % kDistinct;
-            std::vector<uint8_t> mfd(32), mfrd(32 * N), out(up ? 1 : S);
-            std::vector<char> mb(up ? cap : 1);
+            tids[t] = static_cast<long>(syscall(SYS_gettid));
+            std::vector<uint8_t> mfd(32), mfrd(32 * N);
+            HostBuf in, mb, out;  // the handler's request body / Base64 answer / downloaded file
+            in.make(up ? S : 1, pinned);
+            if (up) std::memcpy(in.data(), file[f].data(), S);
+            mb.make(up ? cap : 1, pinned);
+            out.make(up ? 1 : S, pinned);
             std::vector<uint64_t> moff(N + 1);
             std::vector<dfs_span> spans(N);
             for (uint32_t k = 0; k < N; ++k) spans[k] = dfs_span{off[f][k], off[f][k + 1] - off[f][k]};
@@ -123,14 +198,19 @@ int main(int argc, char** argv) {
             while (!go.load()) std::this_thread::yield();
             for (uint64_t it = 0;; ++it) {
                 const auto t0 = Clock::now();
+                const double k0 = thread_cpu_now();
                 int rc;
                 if (up) {
-                    rc = dfs_submit_upload(B, file[f].data(), S, mfd.data(), mfrd.data(), mb.data(), cap, moff.data());
+                    rc = dfs_submit_upload(B, in.data(), S, mfd.data(), mfrd.data(), reinterpret_cast<char*>(mb.data()), cap,
+                                           moff.data());
                 } else {
-                    rc = dfs_submit_download(B, b64[f].data(), spans.data(), S, frd[f].data(), fd[f].data(), out.data());
+                    rc = dfs_submit_download(B, reinterpret_cast<const char*>(text[f].data()), spans.data(), S, frd[f].data(),
+                                             fd[f].data(), out.data());
                 }
                 const auto t1 = Clock::now();
+                const double k1 = thread_cpu_now();
                 if (t0 >= measure_from) lat[t].push_back(std::chrono::duration<double>(t1 - t0).count());
+                if (t0 >= measure_from) cpu_in[t] += k1 - k0;
                 if (rc != DFS_OK) {
                     bad = true;
                     int z = 0;
@@ -141,6 +221,7 @@ int main(int argc, char** argv) {
                     bad = true, ++mismatches;
                 else if (!up && std::memcmp(out.data(), file[f].data(), S))
                     bad = true, ++mismatches;
+                if (t0 >= measure_from) cpu_out[t] += thread_cpu_now() - k1;
                 if (t1 >= deadline) break;
             }
         });
@@ -156,9 +237,15 @@ int main(int argc, char** argv) {
     unsigned long long u0, th0, u1, th1;
     cpu_stat(u0, th0);
     const auto t0 = Clock::now();
+    // client threads exit at the deadline: sample per-thread CPU just before
+    std::this_thread::sleep_until(deadline - dur(0.02));
+    double cpu_cl = 0, cpu_wk = 0, cpu_ot = 0;
+    thread_cpu(tids, cpu_cl, cpu_wk, cpu_ot);
     for (auto& x : th) x.join();
     const double wall = std::chrono::duration<double>(deadline - t0).count();
     cpu_stat(u1, th1);
+    double cin = 0, cout_ = 0;
+    for (int t = 0; t < C; ++t) cin += cpu_in[t], cout_ += cpu_out[t];
     std::vector<double> all;
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());
@@ -167,12 +254,12 @@ int main(int argc, char** argv) {
     dfs_batcher_stats(B, &st);
     dfs_batcher_destroy(B);
     std::printf("{\"clients\": %d, \"kind\": \"%s\", \"requests\": %zu, \"wall_s\": %.4f, \"gbps\": %.4f, "
-                "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"cpu_s\": %.3f, \"throttled_s\": %.3f, \"ok\": %s, \"file0_id\": \"%s\", \"file1_id\": \"%s\", "
-                "\"stats\": {\"batches\": %llu, \"requests\": %llu, \"max_batch\": %llu, \"queue_s\": %.4f, "
+                "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"cpu_s\": %.3f, \"throttled_s\": %.3f, \"cpu_threads_s\": {\"clients\": %.3f, \"workers\": %.3f, \"other\": %.3f}, \"client_cpu_us_per_req\": {\"in_submit\": %.1f, \"outside\": %.1f}, \"ok\": %s, \"file0_id\": \"%s\", \"file1_id\": \"%s\", "
+                "\"pinned\": %d, \"stats\": {\"direct\": %llu, \"batches\": %llu, \"requests\": %llu, \"max_batch\": %llu, \"queue_s\": %.4f, "
                 "\"stage_in_s\": %.4f, \"device_s\": %.4f, \"stage_out_s\": %.4f, \"enqueue_s\": %.4f, \"return_s\": %.4f}}\n",
                 C, up ? "upload" : "download", all.size(), wall, all.size() * static_cast<double>(S) / wall / 1e9,
-                pct(0.5) * 1e3, pct(0.99) * 1e3, (u1 - u0) / 1e6, (th1 - th0) / 1e6, bad ? "false" : "true", hex(fd[0].data()).c_str(),
-                hex(fd[1].data()).c_str(), (unsigned long long)st.batches, (unsigned long long)st.requests,
+                pct(0.5) * 1e3, pct(0.99) * 1e3, (u1 - u0) / 1e6, (th1 - th0) / 1e6, cpu_cl, cpu_wk, cpu_ot, cin / std::max<size_t>(all.size(), 1) * 1e6, cout_ / std::max<size_t>(all.size(), 1) * 1e6, bad ? "false" : "true", hex(fd[0].data()).c_str(),
+                hex(fd[1].data()).c_str(), pinned ? 1 : 0, (unsigned long long)st.direct, (unsigned long long)st.batches, (unsigned long long)st.requests,
                 (unsigned long long)st.max_batch, st.queue_s, st.stage_in_s, st.device_s, st.stage_out_s, st.enqueue_s,
                 st.return_s);
     if (bad)
