@@ -114,7 +114,7 @@ def parse(argv=None):
     ap.add_argument("--store-files", type=int, default=2048, help="files in the on-disk fragment store leg")
     ap.add_argument("--no-store", action="store_true", help="skip the on-disk fragment store leg")
     ap.add_argument("--no-batcher", action="store_true", help="skip the concurrent-clients (batcher) leg")
-    ap.add_argument("--clients", default="1,8,64,512,4096", help="batcher leg: concurrent handler threads")
+    ap.add_argument("--clients", default="1,64,512,2048,4096", help="batcher leg: concurrent handler threads")
     ap.add_argument("--client-seconds", type=float, default=2.0, help="batcher leg: seconds per concurrency")
     ap.add_argument("--long-files", type=int, default=1024)
     ap.add_argument("--long-size", type=int, default=256 << 20)

@@ -158,14 +158,23 @@ int main(int argc, char** argv) {
     std::vector<std::vector<char>> b64(kDistinct);
     std::vector<std::vector<uint64_t>> off(kDistinct, std::vector<uint64_t>(N + 1));
     const uint64_t cap = N * enc_len(S / N + 1) + 16;
-    for (int f = 0; f < kDistinct; ++f) {
-        synth(f, S, file[f].data());
-        b64[f].resize(cap);
-        if (int rc = dfs_submit_upload(B, file[f].data(), S, fd[f].data(), frd[f].data(), b64[f].data(), cap,
-                                       off[f].data())) {
-            std::fprintf(stderr, "warm-up upload: %s\n", dfs_strerror(rc));
-            return 3;
-        }
+    // the distinct files' reference results, uploaded concurrently (one batch)
+    std::atomic<int> warm_rc{0};
+    {
+        std::vector<std::thread> w;
+        for (int f = 0; f < kDistinct; ++f)
+            w.emplace_back([&, f] {
+                synth(f, S, file[f].data());
+                b64[f].resize(cap);
+                if (int rc = dfs_submit_upload(B, file[f].data(), S, fd[f].data(), frd[f].data(), b64[f].data(), cap,
+                                               off[f].data()))
+                    warm_rc = rc;
+            });
+        for (auto& x : w) x.join();
+    }
+    if (warm_rc.load()) {
+        std::fprintf(stderr, "warm-up upload: %s\n", dfs_strerror(warm_rc.load()));
+        return 3;
     }
     std::vector<HostBuf> text(kDistinct);  // the Base64 download clients read (pinned if asked)
     for (int f = 0; f < kDistinct; ++f) {
