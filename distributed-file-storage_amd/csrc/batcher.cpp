@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -51,22 +52,31 @@ using Clock = std::chrono::steady_clock;
 
 uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
 
-// dfs_host_alloc buffers (base -> bytes): a request is direct only if each
-// of its buffers lies inside one of them, so the DMA never touches pageable
-// memory.
+// dfs_host_alloc buffers (base -> bytes, device-mapped base): a request is
+// direct only if each of its buffers lies inside one of them, so the copy
+// kernel never touches pageable memory.
+struct Pinned {
+    uint64_t bytes;
+    uintptr_t dev;  // hipHostGetDevicePointer of the base
+};
 std::shared_mutex g_pin_mu;
-std::map<uintptr_t, uint64_t> g_pinned;
+std::map<uintptr_t, Pinned> g_pinned;
 
-bool in_pinned(const void* p, uint64_t n) {
-    if (!n) return true;
-    if (!p) return false;
+// Device-visible address of host bytes [p, p+n) if they lie in one
+// dfs_host_alloc buffer, else 0 (n == 0: 1, nothing to move).
+uint64_t pinned_dev(const void* p, uint64_t n) {
+    if (!n) return 1;
+    if (!p) return 0;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     std::shared_lock<std::shared_mutex> lk(g_pin_mu);
     auto it = g_pinned.upper_bound(a);
-    if (it == g_pinned.begin()) return false;
+    if (it == g_pinned.begin()) return 0;
     --it;
-    return a - it->first <= it->second && n <= it->second - (a - it->first);
+    const uint64_t o = a - it->first;
+    return o <= it->second.bytes && n <= it->second.bytes - o ? it->second.dev + o : 0;
 }
+bool in_pinned(const void* p, uint64_t n) { return pinned_dev(p, n) != 0; }
+
 
 struct Req;
 
@@ -174,6 +184,29 @@ struct dfs_batcher {
 
 namespace {
 
+// Direct requests' bytes: one DMA per request and direction, except a
+// download's Base64 into HBM, which one copy kernel reads from the handlers'
+// pinned buffers (dfs::copy_spans).  Measured at 4,096 clients
+// (profiles/r02c_batcher/copy_modes.txt): uploads 26.8 GB/s with DMA both
+// ways, 18.8-20.9 with the kernel for either direction (its launch competes
+// with the other workers' kernels); downloads 16.5 with DMA, 17.7-18.9 with
+// the kernel reading the Base64 in.
+int move_in(Worker& w, const std::vector<dfs::CopySpan>& cp, bool kernel) {
+    if (kernel) return dfs::copy_spans(w.ctx, cp.data(), cp.size());
+    for (const auto& c : cp)
+        if (hipMemcpyAsync(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src), c.len, hipMemcpyDefault,
+                           w.stream) != hipSuccess)
+            return DFS_E_HIP;
+    return DFS_OK;
+}
+int move_out(Worker& w, const std::vector<dfs::CopySpan>& cp) {
+    for (const auto& c : cp)
+        if (hipMemcpyAsync(reinterpret_cast<void*>(c.dst), reinterpret_cast<const void*>(c.src), c.len, hipMemcpyDefault,
+                           w.stream) != hipSuccess)
+            return DFS_E_HIP;
+    return DFS_OK;
+}
+
 bool wait_stream(Worker& w) {
     // not hipEventSynchronize: it spins a core for the whole batch (dfs::quiet_wait)
     return hipEventRecord(w.done, w.stream) == hipSuccess && dfs::quiet_wait(w.done) == hipSuccess;
@@ -233,10 +266,12 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
     uint8_t* d_frd = d_fd + 32ull * n;
     if (staged_in && hipMemcpyAsync(w.d_in.p, w.pin_in.p, staged_in, hipMemcpyHostToDevice, w.stream) != hipSuccess)
         return DFS_E_HIP;
-    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i)  // direct: from the handler's pinned buffer
-        if (batch[i]->len && hipMemcpyAsync(w.d_in.as<uint8_t>() + in_off[i], batch[i]->file, batch[i]->len,
-                                            hipMemcpyHostToDevice, w.stream) != hipSuccess)
-            return DFS_E_HIP;
+    std::vector<dfs::CopySpan> cp;  // direct: read from the handlers' pinned buffers
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i)
+        if (batch[i]->len)
+            cp.push_back({pinned_dev(batch[i]->file, batch[i]->len),
+                          reinterpret_cast<uint64_t>(w.d_in.as<uint8_t>() + in_off[i]), batch[i]->len});
+    if (int e = move_in(w, cp, false)) return e;
     // one stream per worker (DFS_SERIAL: the Base64 kernel follows the SHA
     // kernel on it): a box exposes few hardware queues (GPU_MAX_HW_QUEUES=4),
     // and streams sharing one would serialise the workers' batches
@@ -247,12 +282,14 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
     if (hipMemcpyAsync(h, d_fd, dig_bytes, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
         (staged_b64 && hipMemcpyAsync(h + dig_bytes, w.d_out.p, staged_b64, hipMemcpyDeviceToHost, w.stream) != hipSuccess))
         return DFS_E_HIP;
-    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i) {  // direct: into the handler's pinned buffer
+    cp.clear();  // direct: into the handlers' pinned buffers
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i) {
         const Req* r = batch[i];
-        if (r->out_bytes && hipMemcpyAsync(r->b64, w.d_out.as<char>() + b64_off[static_cast<uint64_t>(i) * N],
-                                           r->out_bytes, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
-            return DFS_E_HIP;
+        if (r->out_bytes)
+            cp.push_back({reinterpret_cast<uint64_t>(w.d_out.as<char>() + b64_off[static_cast<uint64_t>(i) * N]),
+                          pinned_dev(r->b64, r->out_bytes), r->out_bytes});
     }
+    if (int e = move_out(w, cp)) return e;
     if (!wait_stream(w)) return DFS_E_HIP;
     tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
@@ -305,27 +342,22 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
     const auto t_dev = Clock::now();
     if (staged_in && hipMemcpyAsync(w.d_in.p, w.pin_in.p, staged_in, hipMemcpyHostToDevice, w.stream) != hipSuccess)
         return DFS_E_HIP;
-    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i) {  // direct: the fragments' Base64, packed
+    std::vector<dfs::CopySpan> cp;  // direct: the fragments' Base64, packed, by one copy kernel
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i) {
         const Req* r = batch[i];
-        uint8_t* d = w.d_in.as<uint8_t>() + in_off[i];
-        const char* run = nullptr;  // fragments back to back in the handler's buffer go as one DMA
-        uint64_t run_len = 0;
-        for (uint32_t k = 0; k <= N; ++k) {
-            const bool end = k == N;
-            const dfs_span sp = end ? dfs_span{0, 0} : r->frags[k];
-            if (!end && (sp.len == DFS_SPAN_MISSING || !sp.len)) continue;
-            if (!end && run && r->text + sp.off == run + run_len) {
-                run_len += sp.len;
-                continue;
-            }
-            if (run_len) {
-                if (hipMemcpyAsync(d, run, run_len, hipMemcpyHostToDevice, w.stream) != hipSuccess) return DFS_E_HIP;
-                d += run_len;
-            }
-            run = end ? nullptr : r->text + sp.off;
-            run_len = end ? 0 : sp.len;
+        uint64_t d = reinterpret_cast<uint64_t>(w.d_in.as<uint8_t>() + in_off[i]);
+        for (uint32_t k = 0; k < N; ++k) {
+            const dfs_span& sp = r->frags[k];
+            if (sp.len == DFS_SPAN_MISSING || !sp.len) continue;
+            const uint64_t src = pinned_dev(r->text + sp.off, sp.len);
+            if (!cp.empty() && cp.back().src + cp.back().len == src && cp.back().dst + cp.back().len == d)
+                cp.back().len += sp.len;  // back to back in the handler's buffer
+            else
+                cp.push_back({src, d, sp.len});
+            d += sp.len;
         }
     }
+    if (int e = move_in(w, cp, true)) return e;
     std::vector<int32_t> st(n);
     rc = dfs_download_batch(w.ctx, w.d_in.as<char>(), spans.data(), n, N, file_len.data(), have_f ? ef.data() : nullptr,
                             have_i ? ei.data() : nullptr, w.d_out.as<uint8_t>(), file_off.data(), st.data(),
@@ -334,11 +366,12 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
         return rc;
     if (staged_out && hipMemcpyAsync(w.pin_out.p, w.d_out.p, staged_out, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
         return DFS_E_HIP;
-    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i)  // direct, good files only (as the staged copy-out)
-        if (st[i] == DFS_OK && batch[i]->len &&
-            hipMemcpyAsync(batch[i]->out, w.d_out.as<uint8_t>() + file_off[i], batch[i]->len, hipMemcpyDeviceToHost,
-                           w.stream) != hipSuccess)
-            return DFS_E_HIP;
+    cp.clear();  // direct, good files only (as the staged copy-out)
+    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i)
+        if (st[i] == DFS_OK && batch[i]->len)
+            cp.push_back({reinterpret_cast<uint64_t>(w.d_out.as<uint8_t>() + file_off[i]),
+                          pinned_dev(batch[i]->out, batch[i]->len), batch[i]->len});
+    if (int e = move_out(w, cp)) return e;
     if (!wait_stream(w)) return DFS_E_HIP;
     tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
@@ -524,12 +557,20 @@ int dfs_host_alloc(uint64_t bytes, void** p) {
     if (!p) return DFS_E_ARG;
     *p = nullptr;
     void* q = nullptr;
-    if (hipHostMalloc(&q, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    // mapped + coherent (fine-grained): the batcher's copy kernel reads and writes it in place, and
+    // the host sees the kernel's writes once the batch's event completes
+    if (hipHostMalloc(&q, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         (void)hipGetLastError();
         return DFS_E_NOMEM;
     }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, q, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        (void)hipHostFree(q);
+        return DFS_E_HIP;
+    }
     std::unique_lock<std::shared_mutex> lk(g_pin_mu);
-    g_pinned[reinterpret_cast<uintptr_t>(q)] = bytes;
+    g_pinned[reinterpret_cast<uintptr_t>(q)] = Pinned{bytes, reinterpret_cast<uintptr_t>(d)};
     *p = q;
     return DFS_OK;
 }

@@ -54,7 +54,7 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_QUEUE, B_COUNT };
+enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_QUEUE, B_COPY, B_COUNT };
 
 }  // namespace
 
@@ -372,6 +372,34 @@ int enter(dfs_ctx* c) {
 }
 
 }  // namespace
+
+namespace dfs {
+int copy_spans(dfs_ctx* c, const CopySpan* spans, size_t n) {
+    if (!c || (n && !spans)) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    hipStream_t s = c->stream();
+    Scratch scratch(c, s);
+    std::vector<StreamJob> jobs;
+    std::vector<uint64_t> items;
+    jobs.reserve(n + 1);
+    items.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (!spans[i].len) continue;
+        StreamJob j{};
+        j.src_off = spans[i].src;
+        j.len = spans[i].len;
+        j.dst_off = spans[i].dst;  // absolute: gather_kernel's output base is 0
+        jobs.push_back(j);
+        items.push_back(copy_items(spans[i].len, static_cast<uintptr_t>(spans[i].dst)));
+    }
+    if (jobs.empty()) return DFS_OK;
+    const uint64_t ntiles = finish_jobs(jobs, items, static_cast<uint64_t>(kGatherPer) * kStreamBlock);
+    if (int rc = put(c, B_COPY, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
+    HIPC(launch_gather(c->buf[B_COPY].as<StreamJob>(), static_cast<uint32_t>(jobs.size() - 1), ntiles, nullptr, s));
+    return DFS_OK;
+}
+}  // namespace dfs
 
 extern "C" {
 

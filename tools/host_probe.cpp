@@ -3,10 +3,13 @@
 //     T threads (a handler's copy in / out of the staging);
 //  2. thread CPU time a caller spends per dfs_upload_batch of one 1 MiB file
 //     (device pointers) + a blocking-sync event wait, i.e. whether any wait
-//     on the path spins.
+//     on the path spins;
+//  3. DMA rate of 512 per-request 1 MiB copies vs one 512 MiB copy, each
+//     way (the batcher's direct path before its copy kernel).
 //   host_probe [threads]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -101,6 +104,55 @@ int main(int argc, char** argv) {
         static const char* names[] = {"blocking-event", "stream-sync", "query-sleep"};
         std::printf("{\"probe\": \"upload_1MiB\", \"wait\": \"%s\", \"wall_ms\": %.3f, \"cpu_call_ms\": %.3f, \"cpu_wait_ms\": %.3f}\n",
                     names[mode], wall / reps * 1e3, cpu_call / reps * 1e3, cpu_wait / reps * 1e3);
+    }
+    // 3. DMA per request vs one DMA per batch: 512 x 1 MiB pinned -> device
+    //    (and 512 x 1.33 MiB back), one stream, as the batcher's direct path.
+    {
+        const int R = 512;
+        const size_t up = n, down = 4 * ((n / 5 + 3) / 3) * 5;
+        void *h_in = nullptr, *h_out = nullptr, *d_a = nullptr, *d_b = nullptr;
+        (void)hipHostMalloc(&h_in, R * up, hipHostMallocDefault);
+        (void)hipHostMalloc(&h_out, R * down, hipHostMallocDefault);
+        (void)hipMalloc(&d_a, R * up);
+        (void)hipMalloc(&d_b, R * down);
+        std::memset(h_in, 1, R * up);
+        for (int mode = 0; mode < 2; ++mode) {
+            double best_h2d = 1e9, best_d2h = 1e9, cpu = 0;
+            for (int rep = 0; rep < 4; ++rep) {
+                (void)hipStreamSynchronize(s);
+                double t0 = now_s(), c0 = thread_cpu_s();
+                if (mode == 0)
+                    for (int r = 0; r < R; ++r)
+                        (void)hipMemcpyAsync(static_cast<char*>(d_a) + r * up, static_cast<char*>(h_in) + r * up, up,
+                                             hipMemcpyHostToDevice, s);
+                else
+                    (void)hipMemcpyAsync(d_a, h_in, R * up, hipMemcpyHostToDevice, s);
+                const double c1 = thread_cpu_s();
+                (void)hipStreamSynchronize(s);
+                double t1 = now_s();
+                if (mode == 0)
+                    for (int r = 0; r < R; ++r)
+                        (void)hipMemcpyAsync(static_cast<char*>(h_out) + r * down, static_cast<char*>(d_b) + r * down,
+                                             down, hipMemcpyDeviceToHost, s);
+                else
+                    (void)hipMemcpyAsync(h_out, d_b, R * down, hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                double t2 = now_s();
+                if (rep) {
+                    best_h2d = std::min(best_h2d, t1 - t0);
+                    best_d2h = std::min(best_d2h, t2 - t1);
+                    cpu += c1 - c0;
+                }
+            }
+            std::printf("{\"probe\": \"dma\", \"mode\": \"%s\", \"requests\": %d, \"h2d_ms\": %.3f, \"h2d_gbs\": %.1f, "
+                        "\"d2h_ms\": %.3f, \"d2h_gbs\": %.1f, \"issue_cpu_ms\": %.3f}\n",
+                        mode ? "one_copy" : "per_request", R, best_h2d * 1e3, R * up / best_h2d / 1e9, best_d2h * 1e3,
+                        R * down / best_d2h / 1e9, cpu / 3 * 1e3);
+        }
+        (void)hipHostFree(h_in);
+        (void)hipHostFree(h_out);
+        (void)hipFree(d_a);
+        (void)hipFree(d_b);
     }
     dfs_close(c);
     return 0;
