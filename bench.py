@@ -114,7 +114,7 @@ def parse(argv=None):
     ap.add_argument("--store-files", type=int, default=2048, help="files in the on-disk fragment store leg")
     ap.add_argument("--no-store", action="store_true", help="skip the on-disk fragment store leg")
     ap.add_argument("--no-batcher", action="store_true", help="skip the concurrent-clients (batcher) leg")
-    ap.add_argument("--clients", default="1,64,512,2048,4096", help="batcher leg: concurrent handler threads")
+    ap.add_argument("--clients", default="1,512,2048,4096", help="batcher leg: concurrent handler threads")
     ap.add_argument("--client-seconds", type=float, default=2.0, help="batcher leg: seconds per concurrency")
     ap.add_argument("--long-files", type=int, default=1024)
     ap.add_argument("--long-size", type=int, default=256 << 20)
@@ -564,6 +564,7 @@ def batcher_leg(args, log):
                 row[key]["device_ms_per_batch"] = round(st["device_s"] / max(st["batches"], 1) * 1e3, 2)
                 row[key]["client_cpu_us_per_req"] = round(r["client_cpu_us_per_req"]["in_submit"], 1)
                 row[key]["cgroup_throttled_s"] = r["throttled_s"]
+                log(f"batcher: {C} clients {key}: {r['gbps']} GB/s p50 {r['p50_ms']} ms")  # progress per run
         th_cpu = min(C, cores)
         nf = max(th_cpu, int(th_cpu / 0.0012))  # ~1 s of work
         secs, _, _ = O.cpu_upload_bench(nf, S, N, th_cpu, use_openssl=True)

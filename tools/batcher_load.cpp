@@ -132,21 +132,32 @@ int main(int argc, char** argv) {
     if (argc > 6) o.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
     if (argc > 7) o.depth = static_cast<uint32_t>(std::atoi(argv[7]));
     const bool pinned = argc > 8 && std::atoi(argv[8]) != 0;
-    // a client buffer: pageable (std::vector) or a dfs_host_alloc buffer
+    // A client buffer: pageable (std::vector) or a slice of one dfs_host_alloc
+    // pool (a server would pin its connection buffers once, not per request;
+    // one pool instead of 3 x C pinned allocations also keeps the setup of
+    // 4,096 clients short).
+    struct Pool {
+        uint8_t* base = nullptr;
+        uint64_t cap = 0;
+        std::atomic<uint64_t> used{0};
+        ~Pool() {
+            if (base) dfs_host_free(base);
+        }
+        uint8_t* take(uint64_t n) {
+            const uint64_t a = used.fetch_add((n + 255) & ~255ull);
+            return base && a + n <= cap ? base + a : nullptr;
+        }
+    } pool;
     struct HostBuf {
         std::vector<uint8_t> v;
-        void* p = nullptr;
-        uint8_t* data() { return p ? static_cast<uint8_t*>(p) : v.data(); }
-        void make(uint64_t n, bool pin) {
-            if (pin && dfs_host_alloc(n ? n : 1, &p) == DFS_OK) return;
+        uint8_t* p = nullptr;
+        uint8_t* data() { return p ? p : v.data(); }
+        void make(uint64_t n, Pool* pl) {
+            if (pl && (p = pl->take(n ? n : 1))) return;
             p = nullptr;
             v.assign(n ? n : 1, 0);
         }
-        ~HostBuf() {
-            if (p) dfs_host_free(p);
-        }
-    };
-    if (C < 1 || N < 1 || N > 64) return 2;
+    };    if (C < 1 || N < 1 || N > 64) return 2;
     dfs_batcher* B = nullptr;
     if (int rc = dfs_batcher_create(0, N, &o, &B)) {
         std::fprintf(stderr, "dfs_batcher_create: %s\n", dfs_strerror(rc));
@@ -176,9 +187,20 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "warm-up upload: %s\n", dfs_strerror(warm_rc.load()));
         return 3;
     }
+    if (pinned) {
+        const uint64_t per = up ? (S + 256) + (cap + 256) + 512 : 256 + 256 + (S + 256);
+        pool.cap = static_cast<uint64_t>(C) * per + kDistinct * (cap + 256);
+        void* q = nullptr;
+        if (dfs_host_alloc(pool.cap, &q) != DFS_OK) {
+            std::fprintf(stderr, "dfs_host_alloc(%llu): out of pinned memory\n", (unsigned long long)pool.cap);
+            return 3;
+        }
+        pool.base = static_cast<uint8_t*>(q);
+    }
+    Pool* pl = pinned ? &pool : nullptr;
     std::vector<HostBuf> text(kDistinct);  // the Base64 download clients read (pinned if asked)
     for (int f = 0; f < kDistinct; ++f) {
-        text[f].make(cap, pinned);
+        text[f].make(cap, pl);
         std::memcpy(text[f].data(), b64[f].data(), cap);
     }
     std::atomic<int> ready{0};
@@ -196,10 +218,10 @@ int main(int argc, char** argv) {
             tids[t] = static_cast<long>(syscall(SYS_gettid));
             std::vector<uint8_t> mfd(32), mfrd(32 * N);
             HostBuf in, mb, out;  // the handler's request body / Base64 answer / downloaded file
-            in.make(up ? S : 1, pinned);
+            in.make(up ? S : 1, pl);
             if (up) std::memcpy(in.data(), file[f].data(), S);
-            mb.make(up ? cap : 1, pinned);
-            out.make(up ? 1 : S, pinned);
+            mb.make(up ? cap : 1, pl);
+            out.make(up ? 1 : S, pl);
             std::vector<uint64_t> moff(N + 1);
             std::vector<dfs_span> spans(N);
             for (uint32_t k = 0; k < N; ++k) spans[k] = dfs_span{off[f][k], off[f][k + 1] - off[f][k]};
