@@ -1,5 +1,7 @@
 #!/bin/bash
 # EXPERIMENT: cost of the SHA kernel's re-reads of misaligned fragment lines.
+# Ran with a temporary DFS_NO_TWINS switch in build_host_plan (not kept in the
+# library; without it the twin lanes change the work between the two sizes).
 # Twins off in every run; S = 1 MiB (fragments at 209,716*i: pairs straddle
 # lines) vs S = 1,048,960 (fragments 128-byte aligned: no shared lines).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
