@@ -419,6 +419,7 @@ const char* dfs_strerror(int code) {
         case DFS_E_WIRE: return "storeFragments body not in buildFragmentsJson form (parse it with parseJson)";
         case DFS_E_IO: return "fragment store I/O error (IOException)";
         case DFS_E_COMM: return dfs_comm_last_error();
+        case DFS_E_TOOBIG: return "batch exceeds the static scratch (dfs_sha256_batch_static: at most 65,536 messages)";
         default: return "unknown error";
     }
 }
@@ -470,6 +471,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_DEC_PRIO")) c->dec_prio = std::atoi(w) ? 1u : 0u;
     if (const char* w = std::getenv("DFS_DEC_WGS")) c->dec_wgs = static_cast<uint32_t>(std::max(1, std::min(8, std::atoi(w))));
     hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = dfs::static_scratch_init(device);  // dfs_sha256_batch_static's device array
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     for (int i = 0; e == hipSuccess && i < 2 * DFS_T_COUNT; ++i) e = hipEventCreate(&c->ev[i]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
@@ -602,6 +604,29 @@ int dfs_sha256_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* msgs, uint
         HIPC(dfs::d2h(c, digests, d_dig, 32ull * n, s));
         HIPC(dfs::quiet_sync(c, s));
     }
+    return DFS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// dfs_sha256_batch for callers that cannot allocate: every buffer is the
+// caller's device memory and the kernels' scratch is the library's static
+// device array (sha256.hip).  No hipMalloc / hipFree, no host staging.
+static_assert(DFS_STATIC_MAX_MSGS == dfs::kStaticMaxMsgs, "header and kernel limits agree");
+int dfs_sha256_batch_static(dfs_ctx* c, const uint8_t* d_base, const dfs_span* d_msgs, uint32_t n, uint8_t* d_digests,
+                            int32_t* d_status) {
+    if (!c || (n && (!d_msgs || !d_digests))) return DFS_E_ARG;
+    if (n > DFS_STATIC_MAX_MSGS) return DFS_E_TOOBIG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!n) return DFS_OK;
+    hipStream_t s = c->stream();
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_SHA, s);
+    HIPC(dfs::launch_sha256_static(c->device, d_base, reinterpret_cast<const uint64_t*>(d_msgs), n, d_digests, d_status,
+                                   c->sha_wps, s));
+    tm.end(DFS_T_SHA, s);
+    tm.end(DFS_T_TOTAL, s);
     return DFS_OK;
 }
 

@@ -170,6 +170,15 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
                          int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr,
                          const ShaWait* wait = nullptr);
+// Allocation-free variant (dfs_sha256_batch_static): descriptors and queue
+// words live in a file-scope device array of sha256.hip, whose address on
+// `device` static_scratch_init resolves once (that device current; called by
+// dfs_open).  d_msgs = n {off, len} pairs in device memory; status (device,
+// may be null) gets 0 or -1 (message of 2^37 bytes or more: hashed as empty).
+constexpr uint32_t kStaticMaxMsgs = 65536;
+hipError_t static_scratch_init(int device);
+hipError_t launch_sha256_static(int device, const uint8_t* base, const uint64_t* d_msgs, uint32_t n, uint8_t* out,
+                                int32_t* status, int waves_per_simd, hipStream_t s);
 // Tiles hold kEncPer*256 12-byte groups (the job table's tile_start must be
 // built with that tile size); prio = s_setprio of the encode waves.
 hipError_t launch_b64_encode(const uint8_t* base, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles,

@@ -877,4 +877,88 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Allocation-free SHA-256 batch (dfs_sha256_batch_static): the lane
+// descriptors and the persistent kernel's queue words live in a file-scope
+// device array instead of the ctx's hipMalloc'ed scratch.  Every GPU holds
+// its own copy of the array until the process ends; its address on a device
+// is resolved once (static_scratch_init, with that device current) and host
+// code uses only that address, never the array's name.  All calls on one GPU
+// share the array: calls that overlap on a GPU race.
+namespace {
+
+constexpr size_t kStaticDescBytes = static_cast<size_t>(kStaticMaxMsgs) * sizeof(ShaDesc);
+static_assert(kStaticDescBytes % 256 == 0, "queue words start 256-byte aligned");
+constexpr size_t kStaticBytes = kStaticDescBytes + kShaQueueBytes;
+
+static __device__ __align__(256) uint8_t scratch[kStaticBytes];
+
+constexpr int kStaticMaxDevices = 64;
+std::mutex g_static_mu;
+void* g_static_ptr[kStaticMaxDevices] = {};
+
+// Span i ({off, len} pairs in device memory) -> lane descriptor i; clears
+// the queue words (a fill kernel, so the sequence may sit in a captured graph).
+__global__ __launch_bounds__(256) void static_prep_kernel(const uint64_t* __restrict__ msgs, uint32_t n,
+                                                         ShaDesc* __restrict__ descs, uint32_t* __restrict__ queue,
+                                                         int32_t* __restrict__ status) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < kShaQueueBytes / 4) queue[i] = 0u;
+    if (i >= n) return;
+    const uint64_t off = msgs[2ull * i], len = msgs[2ull * i + 1];
+    const bool bad = len >= (1ull << 37);  // nfull = len / 64 must fit 32 bits
+    ShaDesc d;
+    d.off = off;
+    d.len = d.total = bad ? 0ull : len;
+    d.out = i;
+    d.flags = 0u;
+    d.b64 = 0ull;
+    descs[i] = d;
+    if (status) status[i] = bad ? -1 : 0;
+}
+
+}  // namespace
+
+hipError_t static_scratch_init(int device) {
+    if (device < 0 || device >= kStaticMaxDevices) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_static_mu);
+    if (g_static_ptr[device]) return hipSuccess;
+    void* p = nullptr;
+    const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(scratch));  // the current device's copy
+    if (e != hipSuccess) return e;
+    if (!p) return hipErrorInvalidSymbol;
+    g_static_ptr[device] = p;
+    return hipSuccess;
+}
+
+hipError_t launch_sha256_static(int device, const uint8_t* base, const uint64_t* d_msgs, uint32_t n, uint8_t* out,
+                                int32_t* status, int waves_per_simd, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (n > kStaticMaxMsgs || device < 0 || device >= kStaticMaxDevices) return hipErrorInvalidValue;
+    uint8_t* ptr;
+    {
+        std::lock_guard<std::mutex> lk(g_static_mu);
+        ptr = static_cast<uint8_t*>(g_static_ptr[device]);
+    }
+    if (!ptr) return hipErrorNotInitialized;
+    ShaDesc* descs = reinterpret_cast<ShaDesc*>(ptr);
+    uint32_t* queue = reinterpret_cast<uint32_t*>(ptr + kStaticDescBytes);
+    const uint32_t work = n > kShaQueueBytes / 4 ? n : static_cast<uint32_t>(kShaQueueBytes / 4);
+    hipLaunchKernelGGL(static_prep_kernel, dim3((work + 255u) / 256u), dim3(256), 0, s, d_msgs, n, descs, queue,
+                       status);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (n <= kChainMaxLanes) {
+        hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, n, out, out,
+                           nullptr);
+    } else {  // unsorted lanes, no long items: every wave pulls from the short queue
+        const uint64_t items = (n + 63u) / 64u;
+        uint64_t waves = 1024ull * static_cast<uint64_t>(waves_per_simd < 1 ? 1 : waves_per_simd);
+        if (waves > items) waves = items;
+        hipLaunchKernelGGL(sha256_lanes, dim3(static_cast<uint32_t>((waves + 3) / 4)), dim3(kShaBlock), 0, s, base,
+                           descs, n, n, 0u, 0u, out, out, queue, nullptr, nullptr, ShaWait{});
+    }
+    return hipGetLastError();
+}
+
 }  // namespace dfs

@@ -28,6 +28,8 @@ DFS_E_NODEV = -8
 DFS_E_WIRE = -9
 DFS_E_IO = -10
 DFS_E_COMM = -11
+DFS_E_TOOBIG = -12
+DFS_STATIC_MAX_MSGS = 65536
 
 DFS_DEVICE_PTRS = 0x1
 DFS_NO_FILEID = 0x2
@@ -92,6 +94,7 @@ SIGNATURES = {
     "dfs_b64_decoded_cap": (_u64, [_u64]),
     "dfs_fragment_holders": (_int, [_u32, _u32, _vp]),
     "dfs_sha256_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _u32]),
+    "dfs_sha256_batch_static": (_int, [_vp, _vp, _vp, _u32, _vp, _vp]),
     "dfs_sha256_update_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _u32]),
     "dfs_receive_fragments_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_b64_encode_batch": (_int, [_vp, _vp, _vp, _u32, _vp, _u64, _vp, _u32]),

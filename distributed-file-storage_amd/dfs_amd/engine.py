@@ -415,6 +415,15 @@ def sha256_device(engine: "FragmentEngine", d_base: int, spans: np.ndarray) -> n
     return dig.view(-1, 32).cpu().numpy()[:n]
 
 
+def sha256_static_device(engine: "FragmentEngine", d_base: int, d_spans: int, n: int, d_digests: int,
+                         d_status: int = 0) -> int:
+    """dfs_sha256_batch_static: every argument a device address (spans
+    included); asynchronous on the engine's stream.  Returns the DFS_* code
+    (DFS_E_TOOBIG beyond DFS_STATIC_MAX_MSGS) instead of raising."""
+    return lib().dfs_sha256_batch_static(engine.ctx, ctypes.c_void_p(d_base or None), ctypes.c_void_p(d_spans or None),
+                                         n, ctypes.c_void_p(d_digests or None), ctypes.c_void_p(d_status or None))
+
+
 def download_device(engine: "FragmentEngine", d_b64: int, spans: np.ndarray, nfiles: int, nfrag: int,
                     file_len: np.ndarray, d_exp_frag: int, d_exp_file: int, d_out: int,
                     file_off: np.ndarray) -> np.ndarray:

@@ -58,6 +58,8 @@ extern "C" {
 #define DFS_E_IO (-10)          /* fragment store: Files.write / readAllBytes      */
                                 /* IOException (SN:166, 285, 466)                 */
 #define DFS_E_COMM (-11)        /* RCCL error (the peer POST failed, SN:218-221)   */
+#define DFS_E_TOOBIG (-12)      /* dfs_sha256_batch_static: more messages than     */
+                                /* DFS_STATIC_MAX_MSGS                             */
 
 /* Flags. */
 #define DFS_DEVICE_PTRS 0x1u    /* data pointers are device pointers; async       */
@@ -123,6 +125,25 @@ int dfs_fragment_holders(uint32_t frag, uint32_t nfrag, uint32_t holders[2]);
  * digests[32*i] = SHA-256(base + msgs[i].off, msgs[i].len). */
 int dfs_sha256_batch(dfs_ctx* ctx, const uint8_t* base, const dfs_span* msgs, uint32_t n,
                      uint8_t* digests, uint32_t flags);
+
+/* dfs_sha256_batch for callers that cannot allocate device memory.  It has no
+ * counterpart in the reference; it exists for code under HIP graph capture,
+ * tight serving loops and harnesses that forbid hipMalloc.  Same digests as
+ * dfs_sha256_batch (sha256Hex, SN:603-613) with DFS_DEVICE_PTRS, but:
+ *  - every argument is device memory, the spans included: d_msgs[i] =
+ *    {off, len} of message i in d_base; d_digests gets n*32 bytes;
+ *  - d_status (n entries, may be NULL) gets 0, or DFS_E_ARG for a message of
+ *    2^37 bytes or more (its digest is then that of the empty message);
+ *  - the lane descriptors and work-queue words live in a static device array
+ *    of the library (about 2.6 MB per GPU, held until the process ends), so
+ *    the call makes no hipMalloc / hipFree and stages nothing on the host;
+ *  - n > DFS_STATIC_MAX_MSGS returns DFS_E_TOOBIG before anything is launched;
+ *  - asynchronous on the ctx stream.  Every call on one GPU (any ctx, any
+ *    process thread) shares that GPU's array: calls that overlap on one GPU
+ *    race, so order them on one stream or with events. */
+#define DFS_STATIC_MAX_MSGS 65536u
+int dfs_sha256_batch_static(dfs_ctx* ctx, const uint8_t* d_base, const dfs_span* d_msgs, uint32_t n,
+                            uint8_t* d_digests, int32_t* d_status);
 
 /* Streaming SHA-256 for messages too long to hold at once (the 256 MiB skew
  * config): each call hashes the next part of every message.
