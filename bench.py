@@ -683,6 +683,7 @@ class Shard:
         C = max(1, min(args.chunks, F))
         bounds = [F * c // C for c in range(C + 1)]
         self.chunks = []
+        raw_max = 0
         for c in range(C):
             a, b = bounds[c], bounds[c + 1]
             spans = np.stack([np.arange(a, b, dtype=np.uint64) * np.uint64(S),
@@ -690,16 +691,29 @@ class Shard:
             plan = dfs_amd.UploadPlan(eng, spans, N, frag_major=True, align128=args.align128)
             offs = plan.b64_offsets()
             grp = [int(offs[f]) for f in range(N)] + [int(offs[-1])]
-            table = comm.sizes([grp[f + 1] - grp[f] for f in range(N)])
+            # replica receiver's plan of this chunk (a collective: every rank's
+            # file lengths are gathered); its table is what dfs_place_sizes gathers
+            rp = P.ReplicaPlan(comm, N, [S] * (b - a), align128=args.align128)
+            table = rp.table
+            if table[comm.rank].tolist() != [grp[f + 1] - grp[f] for f in range(N)]:
+                raise LegError("replica plan: group sizes differ from the upload plan's")
             lay = P.held_layout(comm.world, comm.rank, N, table)
-            ch = {"a": a, "b": b, "plan": plan, "grp": grp, "table": table, "lay": lay,
+            if int(lay[N]) != rp.held_bytes:
+                raise LegError("replica plan: held bytes differ from the placement's")
+            raw_max = max(raw_max, rp.raw_bytes)
+            ch = {"a": a, "b": b, "plan": plan, "grp": grp, "table": table, "lay": lay, "rp": rp,
                   "b64": torch.empty(max(grp[-1], 1), dtype=torch.uint8, device=dev),
                   "held": torch.empty(max(int(lay[N]), 1), dtype=torch.uint8, device=dev),
-                  "ev_up": torch.cuda.Event(), "ev_placed": torch.cuda.Event()}
+                  "verdict": torch.zeros(max(rp.nheld, 1), dtype=torch.int32, device=dev),
+                  "failed": torch.zeros(comm.world, dtype=torch.int32, device=dev),
+                  "ev_up": torch.cuda.Event(), "ev_placed": torch.cuda.Event(), "ev_checked": torch.cuda.Event()}
             for mode in ("ring", "star"):
                 ops, _, _ = P.plan(comm.world, comm.rank, N, table, mode)
                 ch["sent_" + mode] = P.bytes_sent(ops)
             self.chunks.append(ch)
+        # decoded replicas of one chunk (what a holder would write as .frag
+        # files, SN:284-285): one buffer, the chunks' checks run in order
+        self.raw = torch.empty(raw_max + 16, dtype=torch.uint8, device=dev)
         self.fd = torch.empty(F * 32, dtype=torch.uint8, device=dev)
         self.frd = torch.empty(F * N * 32, dtype=torch.uint8, device=dev)
         self.files, self.N = files, N
@@ -738,16 +752,67 @@ def multi_gpu(args, world, rank, local, log):
     torch.cuda.synchronize(dev)
     log(f"{world} ranks x {F} files x {S} B, N={N}, {C} chunks, placement {args.placement}")
 
-    def step(mode, compute=True, place=True):
+    def frd_ptr(ch):
+        return sh.frd.data_ptr() + 32 * N * ch["a"]
+
+    pending = []  # the chunk whose holders' check is still to be enqueued
+
+    def check(ch):
+        """The holder's half of the upload (SN:281-282 + 248-257) on the
+        compute stream: decode + SHA-256 of every held fragment of the chunk,
+        compared with the digests the uploaders sent; then the failure counts
+        back to the uploaders (comm stream)."""
+        s_comp.wait_event(ch["ev_placed"])
+        ch["rp"].check(eng, ch["held"].data_ptr(), sh.raw.data_ptr(), ch["verdict"].data_ptr(),
+                       ch["failed"].data_ptr())
+        ch["ev_checked"].record(s_comp)
+        s_comm.wait_event(ch["ev_checked"])
+        ch["rp"].report(ch["failed"].data_ptr())
+
+    def flush():
+        while pending:
+            check(pending.pop(0))
+
+    def step(mode, compute=True, place=True, verify=True):
+        """One upload of the shard as the reference completes it: hash + encode
+        (compute stream), placement + the digest tables (comm stream), the
+        holders' decode + hash + compare (compute stream) and the failure
+        counts back to the uploaders (comm stream).  The check of a chunk is
+        enqueued one chunk behind the hashing — after the next chunk's upload,
+        which for the last chunk is the next step's first — so its placement
+        hides behind that upload; flush() enqueues what is still pending."""
+        verify = verify and place
         for c, ch in enumerate(sh.chunks):
             if compute:
                 s_comp.wait_event(ch["ev_placed"])  # chunk c's Base64 is free again
                 sh.upload(c, flags)
                 ch["ev_up"].record(s_comp)
             if place:
+                if pending and pending[0] is ch:  # its held buffer is about to be overwritten
+                    flush()
                 s_comm.wait_event(ch["ev_up"])
+                s_comm.wait_event(ch["ev_checked"])  # chunk c's held buffer is free again
                 comm.place(mode, ch["table"], ch["b64"].data_ptr(), ch["held"].data_ptr())
+                if verify:
+                    ch["rp"].exchange(frd_ptr(ch))
                 ch["ev_placed"].record(s_comm)
+            if verify:
+                flush()
+                pending.append(ch)
+
+    def full_steps(mode, n):
+        for _ in range(n):
+            step(mode)
+        flush()  # inside the timed region: the last chunk's check and report
+
+    def verify_only():
+        for ch in sh.chunks:
+            ch["rp"].exchange(frd_ptr(ch))
+            ch["ev_placed"].record(s_comm)
+            check(ch)
+
+    def verify_clean():
+        return all(int(ch["failed"].sum().item()) == 0 and not bool(ch["verdict"].any().item()) for ch in sh.chunks)
 
     def timed(fn, reps):
         torch.cuda.synchronize(dev)
@@ -761,11 +826,44 @@ def multi_gpu(args, world, rank, local, log):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item()) / reps
 
-    for _ in range(args.warmup):
-        step(args.placement)
-    t_step = timed(lambda: step(args.placement), args.steps)
-    # the same step without the exchange, and each placement alone
-    t_comp = timed(lambda: step(args.placement, place=False), max(1, min(args.steps, 3)))
+    full_steps(args.placement, args.warmup)
+    t_step = timed(lambda: full_steps(args.placement, args.steps), 1) / max(args.steps, 1)
+    torch.cuda.synchronize(dev)
+    verify_ok = verify_clean()  # every replica of every step's last run checked good on its holder
+    side = max(1, min(args.steps, 3))
+    # the same step without the holders' verify (round 2's step), without any
+    # exchange, the verify alone, and each placement alone
+    t_noverify = timed(lambda: step(args.placement, verify=False), side)
+    t_comp = timed(lambda: step(args.placement, place=False), side)
+    t_verify = timed(verify_only, side)
+    verify_ok = verify_ok and verify_clean()
+    # A corrupted replica must be caught, by the right holder, for the right
+    # uploader, and every rank must learn of it: rank 0 flips one Base64 char
+    # of one held fragment (to another alphabet char), every rank re-runs the
+    # verify, then the placement restores the held buffer.
+    ch0 = sh.chunks[0]
+    probe = torch.zeros(2, dtype=torch.int64, device=dev)
+    if rank == 0 and ch0["rp"].nheld:
+        fr = ch0["rp"].frags()
+        k = int(ch0["rp"].nheld * 2 // 3)
+        pos = int(fr[k]["b64_off"]) + 5
+        ch0["held"][pos] = ord("B") if int(ch0["held"][pos]) == ord("A") else ord("A")
+        probe[0], probe[1] = k, int(fr[k]["rank"])
+    dist.broadcast(probe, src=0)
+    verify_only()
+    torch.cuda.synchronize(dev)
+    want_failed = torch.zeros(world, dtype=torch.int32, device=dev)
+    want_failed[int(probe[1])] = 1
+    probe_ok = bool(torch.equal(ch0["failed"], want_failed))
+    if rank == 0:
+        bad = torch.nonzero(ch0["verdict"]).flatten().tolist()
+        probe_ok = probe_ok and bad == [int(probe[0])] and int(ch0["verdict"][bad[0]]) == dfs_amd.DFS_E_FRAG_MISMATCH
+    else:
+        probe_ok = probe_ok and not bool(ch0["verdict"].any().item())
+    step(args.placement, compute=False, verify=False)  # restore the held buffer
+    verify_only()
+    torch.cuda.synchronize(dev)
+    verify_ok = verify_ok and probe_ok and verify_clean()
     # SHA-256 kernel time per launch (one launch per chunk), HIP events on
     # the compute stream, outside the timed steps
     eng.set_profiling(True)
@@ -776,8 +874,8 @@ def multi_gpu(args, world, rank, local, log):
     eng.set_profiling(False)
     t_place = {}
     for mode in ("star", "ring"):
-        step(mode, compute=False)
-        t_place[mode] = timed(lambda m=mode: step(m, compute=False), max(1, min(args.steps, 3)))
+        step(mode, compute=False, verify=False)
+        t_place[mode] = timed(lambda m=mode: step(m, compute=False, verify=False), side)
     # held buffers after ring == after star: SHA-256 of every held group
     # (the library's own kernel as a checksum of checksums)
     def held_digests():
@@ -791,9 +889,9 @@ def multi_gpu(args, world, rank, local, log):
         return out
     torch.cuda.synchronize(dev)
     dig_ring = held_digests()
-    step("star", compute=False)
+    step("star", compute=False, verify=False)
     torch.cuda.synchronize(dev)
-    ok = dig_ring == held_digests()
+    ok = dig_ring == held_digests() and verify_ok
     # Degraded read (BASELINE configs[4]): the last GPU offline; every other
     # rank fetches its groups back from the live holders (SN:422-446), then
     # Base64-decodes them into place with per-fragment and fileId verify.
@@ -801,6 +899,9 @@ def multi_gpu(args, world, rank, local, log):
     offline = [world - 1] if world > 1 else []
     fetch_ms = dl_ms = 0.0
     dl_ok = True
+    held_frags = sum(ch["rp"].nheld for ch in sh.chunks)
+    raw_bytes = sum(ch["rp"].raw_bytes for ch in sh.chunks)
+    sh.raw = None  # hand the replica buffer back before the read leg's buffers
     out = torch.empty(max(sh.chunks[0]["b"] - sh.chunks[0]["a"], 1) * S, dtype=torch.uint8, device=dev)
     back = torch.empty(max(ch["grp"][-1] for ch in sh.chunks), dtype=torch.uint8, device=dev)
     for ch in sh.chunks:
@@ -835,6 +936,17 @@ def multi_gpu(args, world, rank, local, log):
             "mode_in_step": args.placement, "chunks": C, "node_to_gpu": "node k on GPU k mod W",
             "compute_only_ms": round(t_comp * 1e3, 3),
             "compute_only_gbps": round(F * S * world / t_comp / 1e9, 3),
+            "receive_verify_ms": round(t_verify * 1e3, 3),
+            "step_without_verify_ms": round(t_noverify * 1e3, 3),
+            "receive_verify": {"held_fragments_per_gpu": held_frags, "decoded_bytes_per_gpu": raw_bytes,
+                               "all_replicas_good": verify_ok, "corrupt_probe_caught": probe_ok,
+                               "note": "inside the timed step: every rank's fragment digests to the holders "
+                                       "(dfs_replica_exchange, RCCL), each holder Base64-decodes and SHA-256s every "
+                                       "held fragment and compares (dfs_replica_check; SN:281-282, 248-257), failure "
+                                       "counts per uploader summed over the holders (dfs_replica_report); "
+                                       "receive_verify_ms = those three alone; the probe flips one held Base64 char on "
+                                       "rank 0 and expects exactly that fragment's DFS_E_FRAG_MISMATCH, counted for its "
+                                       "uploader on every rank"},
             "star_ms": round(t_place["star"] * 1e3, 3),
             "star_xgmi_gbps_per_gpu": round(sent_t[1].item() / world / t_place["star"] / 1e9, 2),
             "ring_ms": round(t_place["ring"] * 1e3, 3),
@@ -851,6 +963,7 @@ def multi_gpu(args, world, rank, local, log):
         "sha_ms_per_launch": float(np.mean(sha_ms)), "files_per_launch": F / C, "ok": ok_all}
     for ch in sh.chunks:
         ch["plan"].close()
+        ch["rp"].close()
     comm.close()
     eng.close()
     eng_c.close()
@@ -984,9 +1097,11 @@ def main():
                 "ms_per_step": round(elapsed * 1e3, 3) if value else None, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None, "dtype": "u32",
                 "data": "synthetic (splitmix64, seed 0x5EED5EED), resident in HBM",
-                "config": {"workload": f"upload + placement: {F} files x {S} B per GPU (BASELINE configs[2] shard), "
-                                       f"N={N} fragments: fileId SHA-256 + fragment SHA-256 + fragment Base64, "
-                                       f"then {args.placement} placement of the Base64 over RCCL/xGMI",
+                "config": {"workload": f"upload + placement + holders' verify: {F} files x {S} B per GPU (BASELINE "
+                                       f"configs[2] shard), N={N} fragments: fileId SHA-256 + fragment SHA-256 + "
+                                       f"fragment Base64, {args.placement} placement of the Base64 over RCCL/xGMI, then "
+                                       f"every holder Base64-decodes and SHA-256s what it received and compares with the "
+                                       f"uploader's digests",
                            "files_per_gpu": F, "file_bytes": S, "nfrag": N, "parallelism": f"files sharded x{world}",
                            "placement": args.placement},
                 "roofline": roofline_n(res, S, N) if ok else None,

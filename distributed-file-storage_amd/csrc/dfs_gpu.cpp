@@ -374,6 +374,12 @@ int enter(dfs_ctx* c) {
 }  // namespace
 
 namespace dfs {
+uint32_t sort_sha_lanes(std::vector<ShaDesc>& d) { return sort_lanes(d); }
+uint64_t finish_stream_jobs(std::vector<StreamJob>& jobs, const std::vector<uint64_t>& items, uint64_t per_tile) {
+    return finish_jobs(jobs, items, per_tile);
+}
+uint64_t decode_items(uint64_t L, uintptr_t dst) { return dec_items(L, dst); }
+
 int copy_spans(dfs_ctx* c, const CopySpan* spans, size_t n) {
     if (!c || (n && !spans)) return DFS_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
@@ -1361,67 +1367,112 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
 }
 
 // ---------------------------------------------------------------------------
-int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32_t nfiles, uint32_t nfrag,
-                       const uint64_t* file_len, const uint8_t* exp_frag, const uint8_t* exp_file, uint8_t* out,
-                       const uint64_t* file_off, int32_t* status, uint32_t flags) {
-    if (!c || !nfrag || (nfiles && (!msgs || !file_len || !out || !file_off || !status))) return DFS_E_ARG;
-    std::lock_guard<std::mutex> lk(c->mu);
-    if (int rc = enter(c)) return rc;
-    Timer tm(c);
-    if (!nfiles) return DFS_OK;
-    const bool dev = flags & DFS_DEVICE_PTRS;
-    hipStream_t s = c->stream();
-    Scratch scratch(c, s);
-    const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
+// Download (Base64 transport): host tables of one batch shape, and the launch
+// sequence over device tables.  dfs_download_batch builds the tables per call
+// into the ctx scratch; a dfs_download_plan builds them once and keeps them in
+// HBM (dfs_download_plan_create / _run).
+}  // extern "C"
+
+struct DlTables {
+    uint32_t nfiles = 0, nfrag = 0;
+    uint64_t nf = 0;          // nfiles * nfrag
+    uint32_t nout = 0;        // digest slots: nf fragments + nfiles fileIds
     uint64_t in_end = 0, out_end = 0;
+    uintptr_t out_align = 0;  // d_out mod 16 the decode tiling was built for
+    bool ovl = false, pipe = false;
+    uint32_t npass = 0, nsha = 0;
+    std::vector<int32_t> status0;  // per file: DFS_OK or DFS_E_MISSING (SN:443-446)
+    std::vector<StreamJob> jobs;   // per-pass tables, then (ovl) groups 1.. with continuous tiles
+    std::vector<ShaDesc> sha;      // per SHA launch: its lanes, then their twins
+    std::vector<uint64_t> gtile;   // ovl: group bounds of the ahead decode
+    std::vector<uint64_t> job0, desc0, tiles;
+    std::vector<uint32_t> prio, nlanes;
+    uint64_t job2 = 0;
+    uint64_t njobs = 0;  // entries of `jobs` (kept when a plan drops the host copy)
+};
+
+// Device side of a download: the tables and the per-run result buffers.
+struct DlDev {
+    const StreamJob* jobs = nullptr;
+    const ShaDesc* desc = nullptr;
+    const uint64_t* gtile = nullptr;
+    int32_t* st = nullptr;       // decode status per fragment
+    int32_t* verdict = nullptr;  // per file (device-resident expected digests)
+    uint8_t* dig = nullptr;      // 32 * (nf + nfiles)
+    uint32_t* queue = nullptr;
+    uint32_t* state = nullptr;   // pipelined passes: running fileId states (32 * nout)
+};
+
+struct dfs_download_plan {
+    int device = 0;
+    DlTables t;
+    DlDev d;
+    void* mem[8] = {};
+};
+
+namespace {
+
+// Decode jobs write straight into the file at the split offsets (fused gather).
+// Large batches, default (overlap): the decode runs fragment by fragment
+// (group g = fragment g of every file): group 0 alone at full width, then
+// groups 1.. beside ONE SHA launch over every lane (fileIds whole, twins),
+// which waits in-kernel for each group's completion count (ShaWait,
+// dfs_internal.h; bounded, the SHA launch is redone after the decode if a
+// wait ever times out).  Pipelined (DFS_DOWNLOAD_MODE=pipelined): passes
+// over fragment groups {0}, {1, 2}, {3..6}, ...:
+// pass p decodes its group of every file on s while the aux stream hashes
+// pass p - 1's fragments and advances every fileId over them (state in
+// HBM between launches, kShaResume / kShaPartial), so the SHA starts after
+// one fragment's decode instead of the whole batch's, and each decode pass
+// runs beside a SHA launch about as long as itself.  A fileId part ends on
+// the last 64-byte boundary inside its group, so it reads decoded bytes only.
+int build_dl_tables(const dfs_ctx* c, const dfs_span* msgs, uint32_t nfiles, uint32_t nfrag, const uint64_t* file_len,
+                    const uint64_t* file_off, uintptr_t out_base, DlTables& t) {
+    t.nfiles = nfiles;
+    t.nfrag = nfrag;
+    const uint64_t nf = static_cast<uint64_t>(nfiles) * nfrag;
+    if (nf + nfiles > 0xffffffffull) return DFS_E_ARG;
+    t.nf = nf;
+    t.nout = static_cast<uint32_t>(nf + nfiles);
+    t.out_align = out_base & 15u;
+    t.status0.assign(nfiles, DFS_OK);
+    std::vector<int32_t>& status = t.status0;
+    t.in_end = t.out_end = 0;
     for (uint32_t f = 0; f < nfiles; ++f) {
-        status[f] = DFS_OK;
         if (file_len[f] >= kMaxMsg) return DFS_E_ARG;
-        out_end = std::max(out_end, file_off[f] + file_len[f]);
+        t.out_end = std::max(t.out_end, file_off[f] + file_len[f]);
         for (uint32_t i = 0; i < nfrag; ++i) {
             const dfs_span& m = msgs[static_cast<uint64_t>(f) * nfrag + i];
             if (m.len == DFS_SPAN_MISSING) status[f] = DFS_E_MISSING;  // SN:443-446
-            else in_end = std::max(in_end, m.off + m.len);
+            else t.in_end = std::max(t.in_end, m.off + m.len);
         }
     }
-    if ((in_end && !b64) || (out_end && !out)) return DFS_E_ARG;
-    const char* d_in = b64;
-    uint8_t* d_out = out;
-    if (!dev) {
-        if (int rc = put(c, B_DATA_IN, b64, in_end, s)) return rc;
-        d_in = c->buf[B_DATA_IN].as<char>();
-        HIPC(c->buf[B_DATA_OUT].ensure(out_end));
-        d_out = c->buf[B_DATA_OUT].as<uint8_t>();
-    }
-    // Decode jobs write straight into the file at the split offsets (fused gather).
-    // Large batches, default (overlap): the decode runs fragment by fragment
-    // (group g = fragment g of every file): group 0 alone at full width, then
-    // groups 1.. beside ONE SHA launch over every lane (fileIds whole, twins),
-    // which waits in-kernel for each group's completion count (ShaWait,
-    // dfs_internal.h; bounded, the SHA launch is redone after the decode if a
-    // wait ever times out).  Pipelined (DFS_DOWNLOAD_MODE=pipelined): passes
-    // over fragment groups {0}, {1, 2}, {3..6}, ...:
-    // pass p decodes its group of every file on s while the aux stream hashes
-    // pass p - 1's fragments and advances every fileId over them (state in
-    // HBM between launches, kShaResume / kShaPartial), so the SHA starts after
-    // one fragment's decode instead of the whole batch's, and each decode pass
-    // runs beside a SHA launch about as long as itself.  A fileId part ends on
-    // the last 64-byte boundary inside its group, so it reads decoded bytes only.
     uint64_t nok = 0;
     for (uint32_t f = 0; f < nfiles; ++f) nok += status[f] == DFS_OK;
     const bool big = nfrag > 1 && nok * (nfrag + 1) > dfs::kChainMaxLanes;
     const bool ovl = big && c->download_mode == 2 && nfrag <= dfs::kShaWaitMaxGroups;
     const bool pipe = big && c->download_mode == 0;
+    t.ovl = ovl;
+    t.pipe = pipe;
     std::vector<uint32_t> gb{0};  // decode group p = fragments [gb[p], gb[p + 1])
     for (uint32_t w = 1; gb.back() < nfrag; w *= 2)
         gb.push_back(ovl ? gb.back() + 1 : (pipe ? std::min(nfrag, gb.back() + w) : nfrag));
     const uint32_t npass = static_cast<uint32_t>(gb.size() - 1);
     const uint32_t nsha = ovl ? 1 : npass;  // SHA launches (overlap: one over every lane)
-    std::vector<StreamJob> jobs, pjobs;
+    t.npass = npass;
+    t.nsha = nsha;
+    std::vector<StreamJob>& jobs = t.jobs;
+    std::vector<StreamJob> pjobs;
     std::vector<uint64_t> items;
-    std::vector<ShaDesc> sha, psha, ptw, gfr;  // per pass: fragments (out = k), files (out = nf + f); twins
-    std::vector<uint64_t> job0(npass + 1, 0), desc0(nsha + 1, 0), tiles(npass);
-    std::vector<uint32_t> prio(nsha), nlanes(nsha);
+    std::vector<ShaDesc>& sha = t.sha;
+    std::vector<ShaDesc> psha, ptw, gfr;  // per pass: fragments (out = k), files (out = nf + f); twins
+    jobs.clear();
+    sha.clear();
+    t.job0.assign(npass + 1, 0);
+    t.desc0.assign(nsha + 1, 0);
+    t.tiles.assign(npass, 0);
+    t.prio.assign(nsha, 0);
+    t.nlanes.assign(nsha, 0);
     std::vector<uint64_t> off(nfrag), len(nfrag);
     // SHA lanes of launch p (fragments [i0, i1)): each file's fileId part,
     // with the fragments that sit on its block grid as twins (twins only if
@@ -1459,12 +1510,12 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
                 j.expect = len[i] + 1;
                 j.id = static_cast<uint32_t>(k);
                 pjobs.push_back(j);
-                items.push_back(dec_items(msgs[k].len, reinterpret_cast<uintptr_t>(d_out + j.dst_off)));
+                items.push_back(dec_items(msgs[k].len, out_base + j.dst_off));
             }
         }
-        tiles[p] = finish_jobs(pjobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
+        t.tiles[p] = finish_jobs(pjobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
         jobs.insert(jobs.end(), pjobs.begin(), pjobs.end());
-        job0[p + 1] = jobs.size();
+        t.job0[p + 1] = jobs.size();
         if (p >= nsha) continue;
         pass_lanes(p, true);
         if (!ptw.empty() && psha.size() < dfs::kTwinMinLanes) pass_lanes(p, false);
@@ -1482,52 +1533,55 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
             for (const ShaDesc& x : psha) gfr[start[key(x)]++] = x;
             psha.swap(gfr);
         }
-        prio[p] = sort_lanes(psha);  // one message per lane, longest first
+        t.prio[p] = sort_lanes(psha);  // one message per lane, longest first
         // Long items (balanced per SIMD, sha256_body): the fileId parts, which
         // are |group| fragments long; in a one-fragment pass every lane is
         // about one fragment long, so every item counts as long.
-        if (pipe) prio[p] = static_cast<uint32_t>(gb[p + 1] - gb[p] == 1 ? psha.size() : nok);
-        nlanes[p] = static_cast<uint32_t>(psha.size());
+        if (pipe) t.prio[p] = static_cast<uint32_t>(gb[p + 1] - gb[p] == 1 ? psha.size() : nok);
+        t.nlanes[p] = static_cast<uint32_t>(psha.size());
         sha.insert(sha.end(), psha.begin(), psha.end());
         sha.insert(sha.end(), ptw.begin(), ptw.end());
-        desc0[p + 1] = sha.size();
+        t.desc0[p + 1] = sha.size();
     }
     // Overlap: groups 1.. as one job table with continuous tile numbers
-    // (jobs2, after the per-group tables in B_JOBS) and group bounds gtile.
-    std::vector<uint64_t> gtile;
-    uint64_t job2 = 0;
+    // (jobs2, after the per-group tables) and group bounds gtile.
+    t.gtile.clear();
+    t.job2 = 0;
     if (ovl) {
-        job2 = jobs.size();
-        uint64_t t = 0;
+        t.job2 = jobs.size();
+        uint64_t tt = 0;
         for (uint32_t p = 1; p < npass; ++p) {
-            gtile.push_back(t);
-            for (uint64_t j = job0[p]; j + 1 < job0[p + 1]; ++j) {  // without the group's sentinel
+            t.gtile.push_back(tt);
+            for (uint64_t j = t.job0[p]; j + 1 < t.job0[p + 1]; ++j) {  // without the group's sentinel
                 StreamJob x = jobs[j];
-                x.tile_start += t;
+                x.tile_start += tt;
                 jobs.push_back(x);
             }
-            t += tiles[p];
+            tt += t.tiles[p];
         }
-        gtile.push_back(t);
+        t.gtile.push_back(tt);
         StreamJob sent{};
-        sent.tile_start = t;
+        sent.tile_start = tt;
         jobs.push_back(sent);
     }
-    if (int rc = put(c, B_JOBS, jobs.data(), jobs.size() * sizeof(StreamJob), s)) return rc;
-    if (int rc = put(c, B_DESC, sha.data(), sha.size() * sizeof(ShaDesc), s)) return rc;
-    if (ovl)
-        if (int rc = put(c, B_JOBS2, gtile.data(), gtile.size() * sizeof(uint64_t), s)) return rc;
-    HIPC(c->buf[B_STATUS].ensure(4ull * nf));
-    HIPC(c->buf[B_OUTLEN].ensure(4ull * nfiles));  // per-file verdicts (device-resident expected digests)
-    HIPC(c->buf[B_DIG0].ensure(32ull * (nf + nfiles)));
-    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
-    HIPC(hipMemsetAsync(c->buf[B_STATUS].p, 0, 4ull * nf, s));
-    uint8_t* d_dig = c->buf[B_DIG0].as<uint8_t>();
-    const StreamJob* d_jobs = c->buf[B_JOBS].as<StreamJob>();
-    const ShaDesc* d_desc = c->buf[B_DESC].as<ShaDesc>();
-    int32_t* d_st = c->buf[B_STATUS].as<int32_t>();
-    uint32_t* d_queue = c->buf[B_QUEUE].as<uint32_t>();
-    const uint32_t nout = static_cast<uint32_t>(nf + nfiles);
+    t.njobs = jobs.size();
+    return DFS_OK;
+}
+
+// Launch sequence + result fetch of one download over device tables.  status
+// must hold the caller's view of t.status0 on entry (DFS_OK / DFS_E_MISSING).
+int run_dl(dfs_ctx* c, const DlTables& t, const DlDev& D, const char* d_in, uint8_t* d_out, const uint8_t* exp_frag,
+           const uint8_t* exp_file, bool dev, uint8_t* host_out, int32_t* status, hipStream_t s, Timer& tm) {
+    const uint32_t nfiles = t.nfiles, nfrag = t.nfrag, npass = t.npass;
+    const uint64_t nf = t.nf;
+    const uint32_t nout = t.nout;
+    const bool ovl = t.ovl, pipe = t.pipe;
+    HIPC(dfs::launch_fill_u32(reinterpret_cast<uint32_t*>(D.st), nf, 0u, s));
+    uint8_t* d_dig = D.dig;
+    const StreamJob* d_jobs = D.jobs;
+    const ShaDesc* d_desc = D.desc;
+    int32_t* d_st = D.st;
+    uint32_t* d_queue = D.queue;
     tm.begin(DFS_T_TOTAL, s);
     if (ovl) {
         if (!c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
@@ -1538,14 +1592,13 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         }
         // The counters live in the SHA queue words, zeroed here (before the
         // decode that publishes them; the SHA launch does not re-zero them).
-        HIPC(hipMemsetAsync(d_queue, 0, dfs::kShaQueueBytes, s));
+        HIPC(dfs::launch_fill_u32(d_queue, dfs::kShaQueueBytes / 4, 0u, s));
         tm.begin(DFS_T_B64DEC, s);
-        HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(job0[1]), tiles[0], d_out, d_st, nullptr, s));
+        HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(t.job0[1]), t.tiles[0], d_out, d_st, nullptr, s));
         HIPC(hipEventRecord(c->pass_ev[0], s));
-        dfs::StreamAhead ah{c->buf[B_JOBS2].as<uint64_t>(), npass - 1, 256u * c->ovl_dec_wgs,
-                         d_queue + dfs::kShaWaitSlot + 1};
-        HIPC(dfs::launch_b64_decode(d_in, d_jobs + job2, static_cast<uint32_t>(jobs.size() - job2), gtile.back(), d_out,
-                                    d_st, nullptr, s, c->dec_prio, 0, &ah));
+        dfs::StreamAhead ah{D.gtile, npass - 1, 256u * c->ovl_dec_wgs, d_queue + dfs::kShaWaitSlot + 1};
+        HIPC(dfs::launch_b64_decode(d_in, d_jobs + t.job2, static_cast<uint32_t>(t.njobs - t.job2), t.gtile.back(),
+                                    d_out, d_st, nullptr, s, c->dec_prio, 0, &ah));
         tm.end(DFS_T_B64DEC, s);
         // The SHA launch waits for group 0 by stream order and for groups
         // 1.. in-kernel.  Launched after the decode it waits on, and sized to
@@ -1553,21 +1606,21 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[0], 0));
         tm.begin(DFS_T_SHA, c->aux);
         const dfs::ShaWait wt{d_queue + dfs::kShaWaitSlot, ah.grid, 1u, nfrag, static_cast<uint32_t>(nf)};
-        HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->ovl_sha_wps,
+        HIPC(dfs::launch_sha256(d_out, d_desc, t.nlanes[0], nout, t.prio[0], d_dig, d_dig, d_queue, c->ovl_sha_wps,
                                 c->aux, nullptr, nullptr, &wt));
         tm.end(DFS_T_SHA, c->aux);
         HIPC(hipEventRecord(c->join, c->aux));
         HIPC(hipStreamWaitEvent(s, c->join, 0));
     } else if (!pipe) {
         tm.begin(DFS_T_B64DEC, s);
-        HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(jobs.size()), tiles[0], d_out, d_st, nullptr, s));
+        HIPC(dfs::launch_b64_decode(d_in, d_jobs, static_cast<uint32_t>(t.njobs), t.tiles[0], d_out, d_st, nullptr,
+                                    s));
         tm.end(DFS_T_B64DEC, s);
         tm.begin(DFS_T_SHA, s);
-        HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
+        HIPC(dfs::launch_sha256(d_out, d_desc, t.nlanes[0], nout, t.prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
         tm.end(DFS_T_SHA, s);
     } else {
-        HIPC(c->buf[B_DIG1].ensure(32ull * nout));  // running fileId states
-        uint32_t* d_state = c->buf[B_DIG1].as<uint32_t>();
+        uint32_t* d_state = D.state;  // running fileId states
         if (!c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
         while (c->pass_ev.size() < npass) {
             hipEvent_t ev = nullptr;
@@ -1576,15 +1629,15 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         }
         tm.begin(DFS_T_B64DEC, s);
         for (uint32_t p = 0; p < npass; ++p) {
-            HIPC(dfs::launch_b64_decode(d_in, d_jobs + job0[p], static_cast<uint32_t>(job0[p + 1] - job0[p]), tiles[p],
-                                        d_out, d_st, nullptr, s, c->dec_prio, p ? c->dec_wgs : 8u));
+            HIPC(dfs::launch_b64_decode(d_in, d_jobs + t.job0[p], static_cast<uint32_t>(t.job0[p + 1] - t.job0[p]),
+                                        t.tiles[p], d_out, d_st, nullptr, s, c->dec_prio, p ? c->dec_wgs : 8u));
             HIPC(hipEventRecord(c->pass_ev[p], s));
         }
         tm.end(DFS_T_B64DEC, s);
         for (uint32_t p = 0; p < npass; ++p) {
             HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[p], 0));
             if (p == 0) tm.begin(DFS_T_SHA, c->aux);
-            HIPC(dfs::launch_sha256(d_out, d_desc + desc0[p], nlanes[p], nout, prio[p], d_dig, d_dig, d_queue,
+            HIPC(dfs::launch_sha256(d_out, d_desc + t.desc0[p], t.nlanes[p], nout, t.prio[p], d_dig, d_dig, d_queue,
                                     c->sha_wps_beside, c->aux, d_state));
         }
         tm.end(DFS_T_SHA, c->aux);
@@ -1600,10 +1653,10 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     auto fetch = [&]() -> int {
         if (dev_verdict) {
             HIPC(dfs::launch_download_verdict(d_st, d_dig, d_dig + 32ull * nf, exp_frag, exp_file, nfiles, nfrag,
-                                              c->buf[B_OUTLEN].as<int32_t>(), s));
-            HIPC(dfs::d2h(c, st.data(), c->buf[B_OUTLEN].p, 4ull * nfiles, s));
+                                              D.verdict, s));
+            HIPC(dfs::d2h(c, st.data(), D.verdict, 4ull * nfiles, s));
         } else {
-            HIPC(dfs::d2h(c, st.data(), c->buf[B_STATUS].p, 4ull * nf, s));
+            HIPC(dfs::d2h(c, st.data(), D.st, 4ull * nf, s));
             HIPC(dfs::d2h(c, dig.data(), d_dig, dig.size(), s));
         }
         return DFS_OK;
@@ -1611,11 +1664,11 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
     uint32_t timed_out = 0;
     if (ovl) HIPC(dfs::d2h(c, &timed_out, d_queue + 2, 4, s));
     if (int e = fetch()) return e;
-    if (!dev && out_end) HIPC(dfs::d2h(c, out, d_out, out_end, s));
+    if (!dev && t.out_end) HIPC(dfs::d2h(c, host_out, d_out, t.out_end, s));
     HIPC(dfs::quiet_sync(c, s));
     if (timed_out) {  // a decode-ahead wait gave up: hash again now that the decode is complete
         ++c->ovl_redo;
-        HIPC(dfs::launch_sha256(d_out, d_desc, nlanes[0], nout, prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
+        HIPC(dfs::launch_sha256(d_out, d_desc, t.nlanes[0], nout, t.prio[0], d_dig, d_dig, d_queue, c->sha_wps, s));
         if (int e = fetch()) return e;
         HIPC(dfs::quiet_sync(c, s));
     }
@@ -1656,6 +1709,136 @@ int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32
         if (status[f] != DFS_OK && rc == DFS_OK) rc = status[f];
     }
     return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfs_download_batch(dfs_ctx* c, const char* b64, const dfs_span* msgs, uint32_t nfiles, uint32_t nfrag,
+                       const uint64_t* file_len, const uint8_t* exp_frag, const uint8_t* exp_file, uint8_t* out,
+                       const uint64_t* file_off, int32_t* status, uint32_t flags) {
+    if (!c || !nfrag || (nfiles && (!msgs || !file_len || !out || !file_off || !status))) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    if (!nfiles) return DFS_OK;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    hipStream_t s = c->stream();
+    Scratch scratch(c, s);
+    // Host-mode output lands in ctx scratch, whose address the tiling needs:
+    // size it first (a download's output never exceeds the sum of its files).
+    uint64_t out_end = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) out_end = std::max(out_end, file_off[f] + file_len[f]);
+    uint8_t* d_out = out;
+    if (!dev) {
+        HIPC(c->buf[B_DATA_OUT].ensure(out_end));
+        d_out = c->buf[B_DATA_OUT].as<uint8_t>();
+    }
+    DlTables t;
+    if (int rc = build_dl_tables(c, msgs, nfiles, nfrag, file_len, file_off, reinterpret_cast<uintptr_t>(d_out), t))
+        return rc;
+    std::memcpy(status, t.status0.data(), 4ull * nfiles);
+    if ((t.in_end && !b64) || (t.out_end && !out)) return DFS_E_ARG;
+    const char* d_in = b64;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, b64, t.in_end, s)) return rc;
+        d_in = c->buf[B_DATA_IN].as<char>();
+    }
+    if (int rc = put(c, B_JOBS, t.jobs.data(), t.jobs.size() * sizeof(StreamJob), s)) return rc;
+    if (int rc = put(c, B_DESC, t.sha.data(), t.sha.size() * sizeof(ShaDesc), s)) return rc;
+    if (t.ovl)
+        if (int rc = put(c, B_JOBS2, t.gtile.data(), t.gtile.size() * sizeof(uint64_t), s)) return rc;
+    HIPC(c->buf[B_STATUS].ensure(4ull * t.nf));
+    HIPC(c->buf[B_OUTLEN].ensure(4ull * nfiles));  // per-file verdicts (device-resident expected digests)
+    HIPC(c->buf[B_DIG0].ensure(32ull * (t.nf + nfiles)));
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    if (t.pipe) HIPC(c->buf[B_DIG1].ensure(32ull * t.nout));
+    DlDev D;
+    D.jobs = c->buf[B_JOBS].as<StreamJob>();
+    D.desc = c->buf[B_DESC].as<ShaDesc>();
+    D.gtile = c->buf[B_JOBS2].as<uint64_t>();
+    D.st = c->buf[B_STATUS].as<int32_t>();
+    D.verdict = c->buf[B_OUTLEN].as<int32_t>();
+    D.dig = c->buf[B_DIG0].as<uint8_t>();
+    D.queue = c->buf[B_QUEUE].as<uint32_t>();
+    D.state = c->buf[B_DIG1].as<uint32_t>();
+    return run_dl(c, t, D, d_in, d_out, exp_frag, exp_file, dev, out, status, s, tm);
+}
+
+// Prepared download: the descriptor tables of one batch shape (spans, file
+// lengths and offsets, N) built once and kept in HBM; run many times on
+// device buffers.  The mode (overlap / pipelined / serial) is the ctx's at
+// creation.
+int dfs_download_plan_create(dfs_ctx* c, const dfs_span* msgs, uint32_t nfiles, uint32_t nfrag,
+                             const uint64_t* file_len, const uint64_t* file_off, dfs_download_plan** out) {
+    if (!c || !out || !nfrag || !nfiles || !msgs || !file_len || !file_off) return DFS_E_ARG;
+    *out = nullptr;
+    auto* p = new (std::nothrow) dfs_download_plan;
+    if (!p) return DFS_E_NOMEM;
+    p->device = c->device;
+    int rc = build_dl_tables(c, msgs, nfiles, nfrag, file_len, file_off, 0, p->t);  // for a 16-byte aligned output
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!rc) rc = enter(c);
+    if (!rc) {
+        const DlTables& t = p->t;
+        const size_t sizes[8] = {std::max<size_t>(t.jobs.size(), 1) * sizeof(StreamJob),
+                                 std::max<size_t>(t.sha.size(), 1) * sizeof(ShaDesc),
+                                 std::max<size_t>(t.gtile.size(), 1) * sizeof(uint64_t),
+                                 std::max<uint64_t>(t.nf, 1) * 4,
+                                 static_cast<size_t>(nfiles) * 4,
+                                 32ull * (t.nf + nfiles),
+                                 dfs::kShaQueueBytes,
+                                 t.pipe ? 32ull * t.nout : 256};
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < 8 && e == hipSuccess; ++i) e = hipMalloc(&p->mem[i], sizes[i]);
+        if (e == hipSuccess && !t.jobs.empty())
+            e = hipMemcpy(p->mem[0], t.jobs.data(), t.jobs.size() * sizeof(StreamJob), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !t.sha.empty())
+            e = hipMemcpy(p->mem[1], t.sha.data(), t.sha.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
+        if (e == hipSuccess && !t.gtile.empty())
+            e = hipMemcpy(p->mem[2], t.gtile.data(), t.gtile.size() * sizeof(uint64_t), hipMemcpyHostToDevice);
+        if (e != hipSuccess) rc = hip_fail(e, "dfs_download_plan_create");
+        p->d.jobs = static_cast<const StreamJob*>(p->mem[0]);
+        p->d.desc = static_cast<const ShaDesc*>(p->mem[1]);
+        p->d.gtile = static_cast<const uint64_t*>(p->mem[2]);
+        p->d.st = static_cast<int32_t*>(p->mem[3]);
+        p->d.verdict = static_cast<int32_t*>(p->mem[4]);
+        p->d.dig = static_cast<uint8_t*>(p->mem[5]);
+        p->d.queue = static_cast<uint32_t*>(p->mem[6]);
+        p->d.state = static_cast<uint32_t*>(p->mem[7]);
+    }
+    if (rc) {
+        dfs_download_plan_destroy(p);
+        return rc;
+    }
+    // the host copies of the big tables are not needed again
+    std::vector<ShaDesc>().swap(p->t.sha);
+    std::vector<StreamJob>().swap(p->t.jobs);
+    *out = p;
+    return DFS_OK;
+}
+
+int dfs_download_plan_destroy(dfs_download_plan* p) {
+    if (!p) return DFS_E_ARG;
+    (void)hipSetDevice(p->device);
+    for (void* m : p->mem)
+        if (m) (void)hipFree(m);
+    delete p;
+    return DFS_OK;
+}
+
+int dfs_download_plan_run(dfs_ctx* c, dfs_download_plan* p, const char* d_b64, const uint8_t* exp_frag,
+                          const uint8_t* exp_file, uint8_t* d_out, int32_t* status) {
+    if (!c || !p || p->device != c->device || !status || !d_out) return DFS_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(d_out) & 15u) != p->t.out_align || (p->t.in_end && !d_b64)) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    hipStream_t s = c->stream();
+    Scratch scratch(c, s);
+    std::memcpy(status, p->t.status0.data(), 4ull * p->t.nfiles);
+    return run_dl(c, p->t, p->d, d_b64, d_out, exp_frag, exp_file, true, nullptr, status, s, tm);
 }
 
 // ---------------------------------------------------------------------------

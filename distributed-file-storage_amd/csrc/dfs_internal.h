@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <mutex>
+#include <vector>
 
 typedef struct dfs_ctx dfs_ctx;
 
@@ -213,6 +214,26 @@ hipError_t launch_download_verdict(const int32_t* dec_status, const uint8_t* fra
                                    int32_t* verdict, hipStream_t s);
 hipError_t launch_synth(uint8_t* dst, const StreamJob* jobs, uint32_t njobs, uint64_t ntiles, uint64_t seed,
                         hipStream_t s, uint64_t file_off);
+
+// Host-side descriptor helpers shared by the entry points (dfs_gpu.cpp):
+// longest-first lane order (returns the lanes of the long items, a multiple
+// of 64), tile_start prefix + sentinel of a job table (returns the tiles),
+// decode work items of one message.
+uint32_t sort_sha_lanes(std::vector<ShaDesc>& d);
+uint64_t finish_stream_jobs(std::vector<StreamJob>& jobs, const std::vector<uint64_t>& items, uint64_t per_tile);
+uint64_t decode_items(uint64_t L, uintptr_t dst);
+
+// Replica receiver (replica.cpp).  fill: n words = v.  transpose: digests
+// [file][frag] -> [frag][file], 32 bytes each.  verdict: held fragment k gets
+// 0 / code_decode (status bit 0) / code_mismatch (status bit 1: wrong length,
+// or got != expected); failed[piece_rank[p]] counts the failures of piece p =
+// held fragments [piece_start[p], piece_start[p + 1]).
+hipError_t launch_fill_u32(uint32_t* p, uint64_t n, uint32_t v, hipStream_t s);
+hipError_t launch_digest_transpose(const uint8_t* in, uint8_t* out, uint32_t nfiles, uint32_t nfrag, hipStream_t s);
+hipError_t launch_replica_verdict(const int32_t* status, const uint8_t* got, const uint8_t* expected, uint64_t n,
+                                  const uint64_t* piece_start, const uint32_t* piece_rank, uint32_t npieces,
+                                  int32_t code_decode, int32_t code_mismatch, int32_t* verdict, uint32_t* failed,
+                                  hipStream_t s);
 
 // ctx internals for the on-disk fragment store (fragstore.cpp).  The store's
 // pinned staging ring lives in the ctx and is freed by dfs_close.

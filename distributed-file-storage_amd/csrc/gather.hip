@@ -120,6 +120,57 @@ __global__ __launch_bounds__(256) void verdict_kernel(const int32_t* __restrict_
     verdict[f] = v;
 }
 
+__global__ __launch_bounds__(256) void fill_u32_kernel(uint32_t* __restrict__ p, uint64_t n, uint32_t v) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// Fragment digests [file][frag] -> [frag][file] (32 bytes each, as two
+// dwordx4): the order in which a rank's digests travel to the holders, group
+// f = fragment f of every file, like its Base64.
+__global__ __launch_bounds__(256) void digest_transpose_kernel(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                               uint32_t nfiles, uint32_t nfrag) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;  // half-digest index in `out`
+    if (i >= 2ull * nfiles * nfrag) return;
+    const uint64_t k = i >> 1;
+    const uint32_t f = static_cast<uint32_t>(k / nfiles), j = static_cast<uint32_t>(k % nfiles);
+    out[i] = in[2ull * (static_cast<uint64_t>(j) * nfrag + f) + (i & 1u)];
+}
+
+// The sender's check of a replica receiver's hashes (SN:248-257), held
+// fragment by held fragment, plus the failures per uploader.
+__global__ __launch_bounds__(256) void replica_verdict_kernel(const int32_t* __restrict__ status,
+                                                              const uint4* __restrict__ got,
+                                                              const uint4* __restrict__ expected, uint64_t n,
+                                                              const uint64_t* __restrict__ piece_start,
+                                                              const uint32_t* __restrict__ piece_rank, uint32_t npieces,
+                                                              int32_t code_decode, int32_t code_mismatch,
+                                                              int32_t* __restrict__ verdict,
+                                                              uint32_t* __restrict__ failed) {
+    const uint64_t k = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+    if (k >= n) return;
+    const int32_t st = status[k];
+    int32_t v = 0;
+    if (st & 1) {
+        v = code_decode;
+    } else {
+        const uint4 a0 = got[2 * k], a1 = got[2 * k + 1], b0 = expected[2 * k], b1 = expected[2 * k + 1];
+        const bool same = a0.x == b0.x && a0.y == b0.y && a0.z == b0.z && a0.w == b0.w && a1.x == b1.x &&
+                          a1.y == b1.y && a1.z == b1.z && a1.w == b1.w;
+        if ((st & 2) || !same) v = code_mismatch;
+    }
+    if (verdict) verdict[k] = v;
+    if (v) {
+        uint32_t lo = 0, hi = npieces;  // piece_start[lo] <= k < piece_start[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (piece_start[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        atomicAdd(failed + piece_rank[lo], 1u);
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -166,6 +217,31 @@ hipError_t launch_download_verdict(const int32_t* dec_status, const uint8_t* fra
     if (nfiles == 0) return hipSuccess;
     hipLaunchKernelGGL(verdict_kernel, dim3((nfiles + 255) / 256), dim3(256), 0, s, dec_status, frag_dig, file_dig,
                        exp_frag, exp_file, nfiles, nfrag, verdict);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_u32(uint32_t* p, uint64_t n, uint32_t v, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_u32_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, p, n, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_digest_transpose(const uint8_t* in, uint8_t* out, uint32_t nfiles, uint32_t nfrag, hipStream_t s) {
+    const uint64_t n = 2ull * nfiles * nfrag;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(digest_transpose_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint4*>(in), reinterpret_cast<uint4*>(out), nfiles, nfrag);
+    return hipGetLastError();
+}
+
+hipError_t launch_replica_verdict(const int32_t* status, const uint8_t* got, const uint8_t* expected, uint64_t n,
+                                  const uint64_t* piece_start, const uint32_t* piece_rank, uint32_t npieces,
+                                  int32_t code_decode, int32_t code_mismatch, int32_t* verdict, uint32_t* failed,
+                                  hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(replica_verdict_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, status,
+                       reinterpret_cast<const uint4*>(got), reinterpret_cast<const uint4*>(expected), n, piece_start,
+                       piece_rank, npieces, code_decode, code_mismatch, verdict, failed);
     return hipGetLastError();
 }
 

@@ -35,10 +35,15 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <string>
 #include <vector>
+
+#include <map>
+#include <utility>
 
 #include "../../include/dfs_gpu.h"
 #include "dfs_internal.h"
+#include "placement_internal.h"
 
 static_assert(DFS_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
@@ -47,12 +52,18 @@ struct dfs_comm {
     ncclComm_t nc = nullptr;
     uint32_t nranks = 0, rank = 0;
     uint64_t* d_sizes = nullptr;  // all-gather scratch (nranks * kMaxFrag words)
+    uint64_t* d_gather = nullptr; // allgather_u64 scratch
+    uint64_t gather_cap = 0;      // words
 };
 
-namespace {
+using dfs::holder_a;
+using dfs::holder_b;
+using dfs::holds;
+using dfs::kMaxFrag;
+using dfs::kMaxRanks;
+using dfs::Plan;
 
-constexpr uint32_t kMaxFrag = 64;
-constexpr uint32_t kMaxRanks = 64;  // offline masks are 64-bit
+namespace {
 
 thread_local char g_last_comm[160];
 
@@ -70,17 +81,6 @@ int comm_fail(ncclResult_t r, const char* what) {
     do {                                                \
         if ((x) != hipSuccess) return DFS_E_HIP;        \
     } while (0)
-
-uint32_t holder_a(uint32_t f, uint32_t N, uint32_t W) { return f % W; }                  // node f (SN:427)
-uint32_t holder_b(uint32_t f, uint32_t N, uint32_t W) { return ((f + N - 1) % N) % W; }  // node f-1 (SN:428)
-bool holds(uint32_t g, uint32_t f, uint32_t N, uint32_t W) { return holder_a(f, N, W) == g || holder_b(f, N, W) == g; }
-
-struct Plan {
-    std::vector<dfs_xfer> ops;
-    std::vector<uint64_t> dst_off;  // nfrag + 1
-    std::vector<int32_t> status;    // nfrag
-    uint32_t phases = 0;
-};
 
 // Bytes of rank r's group f.
 inline uint64_t T(const uint64_t* table, uint32_t N, uint32_t r, uint32_t f) { return table[static_cast<uint64_t>(r) * N + f]; }
@@ -100,7 +100,9 @@ void add(Plan& p, uint32_t phase, uint32_t kind, int32_t peer, uint32_t f, uint3
     p.ops.push_back(x);
 }
 
-int build_plan(uint32_t W, uint32_t me, uint32_t N, const uint64_t* table, uint32_t mode, uint64_t offline, Plan& p) {
+}  // namespace
+
+int dfs::build_plan(uint32_t W, uint32_t me, uint32_t N, const uint64_t* table, uint32_t mode, uint64_t offline, Plan& p) {
     if (!W || W > kMaxRanks || me >= W || !N || N > kMaxFrag || !table) return DFS_E_ARG;
     if (mode > DFS_PLACE_FETCH) return DFS_E_ARG;
     p.ops.clear();
@@ -200,57 +202,88 @@ int build_plan(uint32_t W, uint32_t me, uint32_t N, const uint64_t* table, uint3
     return DFS_OK;
 }
 
-// Issue one plan per comm (ncomms > 1: one process driving several GPUs,
-// every comm's ops inside the same group per phase).
-int run_plans(dfs_comm* const* comms, uint32_t ncomms, const std::vector<Plan>& plans, const void* const* src,
-              void* const* dst) {
+namespace dfs {
+
+int run_plans(Transport& t, const std::vector<Plan>& plans, const void* const* src, void* const* dst) {
+    const uint32_t n = static_cast<uint32_t>(plans.size());
     uint32_t phases = 0;
     for (const Plan& p : plans) phases = p.phases > phases ? p.phases : phases;
     for (uint32_t ph = 0; ph < phases; ++ph) {
         // local copies first (same stream as the group: ordered before it)
-        for (uint32_t i = 0; i < ncomms; ++i) {
-            HIPCHK(hipSetDevice(dfs::ctx_device(comms[i]->ctx)));
-            hipStream_t s = dfs::ctx_stream(comms[i]->ctx);
+        for (uint32_t i = 0; i < n; ++i)
             for (const dfs_xfer& x : plans[i].ops) {
                 if (x.phase != ph || x.kind != DFS_XFER_COPY) continue;
                 const char* from = x.from_dst ? static_cast<const char*>(dst[i]) : static_cast<const char*>(src[i]);
-                HIPCHK(hipMemcpyAsync(static_cast<char*>(dst[i]) + x.dst_off, from + x.src_off, x.len,
-                                      hipMemcpyDeviceToDevice, s));
+                if (int rc = t.copy(i, static_cast<char*>(dst[i]) + x.dst_off, from + x.src_off, x.len)) return rc;
             }
-        }
         bool any = false;
-        for (uint32_t i = 0; i < ncomms && !any; ++i)
+        for (uint32_t i = 0; i < n && !any; ++i)
             for (const dfs_xfer& x : plans[i].ops)
                 if (x.phase == ph && x.kind != DFS_XFER_COPY) {
                     any = true;
                     break;
                 }
         if (!any) continue;
-        NCCLC(ncclGroupStart());
-        for (uint32_t i = 0; i < ncomms; ++i) {
-            if (ncomms > 1 && hipSetDevice(dfs::ctx_device(comms[i]->ctx)) != hipSuccess) {
-                (void)ncclGroupEnd();
-                return DFS_E_HIP;
-            }
-            hipStream_t s = dfs::ctx_stream(comms[i]->ctx);
+        if (int rc = t.group_start()) return rc;
+        for (uint32_t i = 0; i < n; ++i)
             for (const dfs_xfer& x : plans[i].ops) {
                 if (x.phase != ph || x.kind == DFS_XFER_COPY) continue;
-                ncclResult_t r;
+                int rc;
                 if (x.kind == DFS_XFER_SEND) {
                     const char* from = x.from_dst ? static_cast<const char*>(dst[i]) : static_cast<const char*>(src[i]);
-                    r = ncclSend(from + x.src_off, x.len, ncclUint8, x.peer, comms[i]->nc, s);
+                    rc = t.send(i, from + x.src_off, x.len, x.peer);
                 } else {
-                    r = ncclRecv(static_cast<char*>(dst[i]) + x.dst_off, x.len, ncclUint8, x.peer, comms[i]->nc, s);
+                    rc = t.recv(i, static_cast<char*>(dst[i]) + x.dst_off, x.len, x.peer);
                 }
-                if (r != ncclSuccess) {
-                    (void)ncclGroupEnd();
-                    return comm_fail(r, x.kind == DFS_XFER_SEND ? "ncclSend" : "ncclRecv");
+                if (rc) {
+                    (void)t.group_end();
+                    return rc;
                 }
             }
-        }
-        NCCLC(ncclGroupEnd());
+        if (int rc = t.group_end()) return rc;
     }
     return DFS_OK;
+}
+
+// RCCL: every op on its comm's ctx stream, sends and receives of a phase
+// inside one ncclGroupStart / End.
+struct RcclTransport : Transport {
+    dfs_comm* const* comms;
+    uint32_t ncomms;
+    RcclTransport(dfs_comm* const* c, uint32_t n) : comms(c), ncomms(n) {}
+    int use(uint32_t i) {
+        HIPCHK(hipSetDevice(dfs::ctx_device(comms[i]->ctx)));
+        return DFS_OK;
+    }
+    int copy(uint32_t i, void* dst, const void* src, uint64_t n) override {
+        if (int rc = use(i)) return rc;
+        HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, dfs::ctx_stream(comms[i]->ctx)));
+        return DFS_OK;
+    }
+    int group_start() override {
+        NCCLC(ncclGroupStart());
+        return DFS_OK;
+    }
+    int send(uint32_t i, const void* p, uint64_t n, int32_t peer) override {
+        if (int rc = use(i)) return rc;
+        const ncclResult_t r = ncclSend(p, n, ncclUint8, peer, comms[i]->nc, dfs::ctx_stream(comms[i]->ctx));
+        return r == ncclSuccess ? DFS_OK : comm_fail(r, "ncclSend");
+    }
+    int recv(uint32_t i, void* p, uint64_t n, int32_t peer) override {
+        if (int rc = use(i)) return rc;
+        const ncclResult_t r = ncclRecv(p, n, ncclUint8, peer, comms[i]->nc, dfs::ctx_stream(comms[i]->ctx));
+        return r == ncclSuccess ? DFS_OK : comm_fail(r, "ncclRecv");
+    }
+    int group_end() override {
+        NCCLC(ncclGroupEnd());
+        return DFS_OK;
+    }
+};
+
+int run_plans_rccl(dfs_comm* const* comms, uint32_t ncomms, const std::vector<Plan>& plans, const void* const* src,
+                   void* const* dst) {
+    RcclTransport t(comms, ncomms);
+    return run_plans(t, plans, src, dst);
 }
 
 int check_comms(dfs_comm* const* comms, uint32_t ncomms) {
@@ -260,19 +293,186 @@ int check_comms(dfs_comm* const* comms, uint32_t ncomms) {
     return DFS_OK;
 }
 
+dfs_ctx* comm_ctx(const dfs_comm* c) { return c->ctx; }
+
+int allreduce_u32(dfs_comm* const* comms, uint32_t ncomms, uint32_t* const* d_buf, uint32_t count) {
+    NCCLC(ncclGroupStart());
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        dfs_comm* c = comms[i];
+        ncclResult_t r = ncclSuccess;
+        if (hipSetDevice(dfs::ctx_device(c->ctx)) != hipSuccess) r = ncclUnhandledCudaError;
+        if (r == ncclSuccess) r = ncclAllReduce(d_buf[i], d_buf[i], count, ncclUint32, ncclSum, c->nc, dfs::ctx_stream(c->ctx));
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return comm_fail(r, "ncclAllReduce");
+        }
+    }
+    NCCLC(ncclGroupEnd());
+    return DFS_OK;
+}
+
+int allgather_u64(dfs_comm* const* comms, uint32_t ncomms, const uint64_t* const* mine, uint64_t count,
+                  uint64_t* const* all) {
+    if (!count) return DFS_OK;
+    const uint32_t W = comms[0]->nranks;
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        dfs_comm* c = comms[i];
+        HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
+        const uint64_t need = (static_cast<uint64_t>(W) + 1) * count;
+        if (c->gather_cap < need) {
+            if (c->d_gather) (void)hipFree(c->d_gather);
+            c->d_gather = nullptr;
+            c->gather_cap = 0;
+            HIPCHK(hipMalloc(&c->d_gather, 8 * need));
+            c->gather_cap = need;
+        }
+        HIPCHK(hipMemcpyAsync(c->d_gather + static_cast<uint64_t>(W) * count, mine[i], 8 * count, hipMemcpyHostToDevice,
+                              dfs::ctx_stream(c->ctx)));
+    }
+    NCCLC(ncclGroupStart());
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        dfs_comm* c = comms[i];
+        ncclResult_t r = ncclSuccess;
+        if (hipSetDevice(dfs::ctx_device(c->ctx)) != hipSuccess) r = ncclUnhandledCudaError;
+        if (r == ncclSuccess)
+            r = ncclAllGather(c->d_gather + static_cast<uint64_t>(W) * count, c->d_gather, count, ncclUint64, c->nc,
+                              dfs::ctx_stream(c->ctx));
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return comm_fail(r, "ncclAllGather");
+        }
+    }
+    NCCLC(ncclGroupEnd());
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        dfs_comm* c = comms[i];
+        HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
+        HIPCHK(hipMemcpyAsync(all[i], c->d_gather, 8ull * W * count, hipMemcpyDeviceToHost, dfs::ctx_stream(c->ctx)));
+    }
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        HIPCHK(hipSetDevice(dfs::ctx_device(comms[i]->ctx)));
+        HIPCHK(hipStreamSynchronize(dfs::ctx_stream(comms[i]->ctx)));
+    }
+    return DFS_OK;
+}
+
+}  // namespace dfs
+
+namespace {
+
+using dfs::check_comms;
+
+// In-process stand-in for RCCL's group semantics over host memory, one
+// endpoint per rank: what a group posts is held until group_end, which pairs
+// rank a's sends to b with b's receives from a in posting order, requires
+// equal counts and equal sizes (RCCL would hang or corrupt otherwise), rejects
+// a group in which a send reads bytes that a receive or another send's peer
+// writes in the same group (their order is undefined on the wire), and only
+// then moves the bytes.
+struct SimTransport : dfs::Transport {
+    struct Op {
+        const char* src = nullptr;
+        char* dst = nullptr;
+        uint64_t n = 0;
+    };
+    uint32_t W;
+    bool open = false;
+    std::map<std::pair<uint32_t, uint32_t>, std::vector<Op>> sends, recvs;  // key = (from, to)
+    std::string err;
+    explicit SimTransport(uint32_t w) : W(w) {}
+    int fail(const std::string& m) {
+        err = m;
+        std::snprintf(g_last_comm, sizeof g_last_comm, "simulated exchange: %s", m.c_str());
+        return DFS_E_COMM;
+    }
+    int copy(uint32_t, void* dst, const void* src, uint64_t n) override {
+        if (open) return fail("copy inside a group");
+        std::memmove(dst, src, n);
+        return DFS_OK;
+    }
+    int group_start() override {
+        if (open) return fail("nested group");
+        open = true;
+        sends.clear();
+        recvs.clear();
+        return DFS_OK;
+    }
+    int send(uint32_t i, const void* p, uint64_t n, int32_t peer) override {
+        if (!open || peer < 0 || static_cast<uint32_t>(peer) >= W || static_cast<uint32_t>(peer) == i)
+            return fail("bad send");
+        Op o;
+        o.src = static_cast<const char*>(p);
+        o.n = n;
+        sends[{i, static_cast<uint32_t>(peer)}].push_back(o);
+        return DFS_OK;
+    }
+    int recv(uint32_t i, void* p, uint64_t n, int32_t peer) override {
+        if (!open || peer < 0 || static_cast<uint32_t>(peer) >= W || static_cast<uint32_t>(peer) == i)
+            return fail("bad recv");
+        Op o;
+        o.dst = static_cast<char*>(p);
+        o.n = n;
+        recvs[{static_cast<uint32_t>(peer), i}].push_back(o);
+        return DFS_OK;
+    }
+    int group_end() override {
+        if (!open) return fail("group_end without group_start");
+        open = false;
+        char buf[128];
+        for (const auto& kv : recvs)
+            if (!sends.count(kv.first)) {
+                std::snprintf(buf, sizeof buf, "%u receives from rank %u on rank %u without a send", static_cast<unsigned>(kv.second.size()),
+                              kv.first.first, kv.first.second);
+                return fail(buf);
+            }
+        std::vector<Op> moves;
+        for (const auto& kv : sends) {
+            const auto it = recvs.find(kv.first);
+            const size_t nr = it == recvs.end() ? 0 : it->second.size();
+            if (nr != kv.second.size()) {
+                std::snprintf(buf, sizeof buf, "rank %u -> %u: %u sends vs %u receives", kv.first.first, kv.first.second,
+                              static_cast<unsigned>(kv.second.size()), static_cast<unsigned>(nr));
+                return fail(buf);
+            }
+            for (size_t k = 0; k < nr; ++k) {
+                if (kv.second[k].n != it->second[k].n) {
+                    std::snprintf(buf, sizeof buf, "rank %u -> %u op %u: send %llu bytes vs receive %llu", kv.first.first,
+                                  kv.first.second, static_cast<unsigned>(k), static_cast<unsigned long long>(kv.second[k].n),
+                                  static_cast<unsigned long long>(it->second[k].n));
+                    return fail(buf);
+                }
+                Op m;
+                m.src = kv.second[k].src;
+                m.dst = it->second[k].dst;
+                m.n = kv.second[k].n;
+                moves.push_back(m);
+            }
+        }
+        // no read of bytes written in the same group, no two writes to the same bytes
+        for (size_t a = 0; a < moves.size(); ++a)
+            for (size_t b = 0; b < moves.size(); ++b) {
+                const Op &x = moves[a], &y = moves[b];
+                if (!x.n || !y.n) continue;
+                if (x.src < y.dst + y.n && y.dst < x.src + x.n) return fail("a send reads bytes a receive of the same group writes");
+                if (a < b && x.dst < y.dst + y.n && y.dst < x.dst + x.n) return fail("two receives of one group overlap");
+            }
+        for (const Op& m : moves) std::memcpy(m.dst, m.src, m.n);
+        return DFS_OK;
+    }
+};
+
 int place(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table, uint32_t mode,
           uint64_t offline, const void* const* src, void* const* dst, int32_t* frag_status) {
     if (int rc = check_comms(comms, ncomms)) return rc;
     if (!src || !dst) return DFS_E_ARG;
     std::vector<Plan> plans(ncomms);
     for (uint32_t i = 0; i < ncomms; ++i) {
-        if (int rc = build_plan(comms[i]->nranks, comms[i]->rank, nfrag, table, mode, offline, plans[i])) return rc;
+        if (int rc = dfs::build_plan(comms[i]->nranks, comms[i]->rank, nfrag, table, mode, offline, plans[i])) return rc;
         if (plans[i].dst_off[nfrag] && !dst[i]) return DFS_E_ARG;
         for (const dfs_xfer& x : plans[i].ops)
             if (x.kind != DFS_XFER_RECV && !x.from_dst && !src[i]) return DFS_E_ARG;
         if (frag_status) std::memcpy(frag_status + static_cast<uint64_t>(i) * nfrag, plans[i].status.data(), 4ull * nfrag);
     }
-    return run_plans(comms, ncomms, plans, src, dst);
+    return dfs::run_plans_rccl(comms, ncomms, plans, src, dst);
 }
 
 }  // namespace
@@ -285,7 +485,7 @@ int dfs_place_plan(uint32_t nranks, uint32_t rank, uint32_t nfrag, const uint64_
                    uint64_t offline_mask, dfs_xfer* ops, uint32_t* nops, uint64_t* dst_off, int32_t* frag_status) {
     if (!nops) return DFS_E_ARG;
     Plan p;
-    if (int rc = build_plan(nranks, rank, nfrag, table, mode, offline_mask, p)) return rc;
+    if (int rc = dfs::build_plan(nranks, rank, nfrag, table, mode, offline_mask, p)) return rc;
     const uint32_t cap = *nops;
     *nops = static_cast<uint32_t>(p.ops.size());
     if (dst_off) std::memcpy(dst_off, p.dst_off.data(), 8ull * (nfrag + 1));
@@ -295,6 +495,21 @@ int dfs_place_plan(uint32_t nranks, uint32_t rank, uint32_t nfrag, const uint64_
         std::memcpy(ops, p.ops.data(), sizeof(dfs_xfer) * p.ops.size());
     }
     return DFS_OK;
+}
+
+int dfs_place_simulate(uint32_t nranks, uint32_t nfrag, const uint64_t* table, uint32_t mode, uint64_t offline_mask,
+                       const uint8_t* const* src, uint8_t* const* dst, int32_t* frag_status) {
+    if (!nranks || nranks > kMaxRanks || !src || !dst) return DFS_E_ARG;
+    std::vector<Plan> plans(nranks);
+    for (uint32_t r = 0; r < nranks; ++r) {
+        if (int rc = dfs::build_plan(nranks, r, nfrag, table, mode, offline_mask, plans[r])) return rc;
+        if (plans[r].dst_off[nfrag] && !dst[r]) return DFS_E_ARG;
+        for (const dfs_xfer& x : plans[r].ops)
+            if (x.kind != DFS_XFER_RECV && !x.from_dst && !src[r]) return DFS_E_ARG;
+        if (frag_status) std::memcpy(frag_status + static_cast<uint64_t>(r) * nfrag, plans[r].status.data(), 4ull * nfrag);
+    }
+    SimTransport t(nranks);
+    return dfs::run_plans(t, plans, reinterpret_cast<const void* const*>(src), reinterpret_cast<void* const*>(dst));
 }
 
 int dfs_comm_unique_id(uint8_t* id) {
@@ -360,6 +575,7 @@ int dfs_comm_destroy(dfs_comm* c) {
     (void)hipStreamSynchronize(dfs::ctx_stream(c->ctx));
     if (c->nc) (void)ncclCommDestroy(c->nc);
     if (c->d_sizes) (void)hipFree(c->d_sizes);
+    if (c->d_gather) (void)hipFree(c->d_gather);
     delete c;
     return DFS_OK;
 }

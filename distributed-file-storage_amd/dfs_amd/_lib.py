@@ -74,6 +74,10 @@ XFER_DTYPE = [("phase", "<u4"), ("kind", "<u4"), ("peer", "<i4"), ("frag", "<u4"
               ("reserved", "<u4"), ("src_off", "<u8"), ("dst_off", "<u8"), ("len", "<u8")]
 
 
+# dfs_held_frag (48 bytes).
+HELD_FRAG_DTYPE = [("rank", "<u4"), ("file", "<u4"), ("frag", "<u4"), ("reserved", "<u4"), ("b64_off", "<u8"),
+                   ("b64_len", "<u8"), ("raw_off", "<u8"), ("raw_len", "<u8")]
+
 _vp = ctypes.c_void_p
 _u32 = ctypes.c_uint32
 _u64 = ctypes.c_uint64
@@ -102,6 +106,9 @@ SIGNATURES = {
     "dfs_upload_batch": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _u64, _vp, _u32]),
     "dfs_reassemble_verify": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _u32]),
     "dfs_download_batch": (_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    "dfs_download_plan_create": (_int, [_vp, _vp, _u32, _u32, _vp, _vp, ctypes.POINTER(_vp)]),
+    "dfs_download_plan_run": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "dfs_download_plan_destroy": (_int, [_vp]),
     "dfs_upload_plan_create": (_int, [_vp, _vp, _u32, _u32, _u32, ctypes.POINTER(_vp), ctypes.POINTER(_u64)]),
     "dfs_upload_plan_b64_offsets": (_int, [_vp, _vp]),
     "dfs_upload_plan_run": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _u32]),
@@ -132,6 +139,16 @@ SIGNATURES = {
     "dfs_place_ring": (_int, [_vp, _u32, _u32, _vp, _vp, _vp]),
     "dfs_place_star": (_int, [_vp, _u32, _u32, _vp, _vp, _vp]),
     "dfs_fetch_degraded": (_int, [_vp, _u32, _u32, _vp, _u64, _vp, _vp, _vp]),
+    "dfs_place_simulate": (_int, [_u32, _u32, _vp, _u32, _u64, _vp, _vp, _vp]),
+    "dfs_replica_layout": (_int, [_u32, _u32, _u32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "dfs_replica_plan_create": (_int, [_vp, _u32, _u32, _vp, _vp, _u32, _vp]),
+    "dfs_replica_plan_info": (_int, [_vp, _vp, _vp, _vp, _vp]),
+    "dfs_replica_plan_frags": (_int, [_vp, _vp]),
+    "dfs_replica_verify": (_int, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "dfs_replica_exchange": (_int, [_vp, _u32, _vp, _vp]),
+    "dfs_replica_check": (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "dfs_replica_report": (_int, [_vp, _u32, _vp]),
+    "dfs_replica_plan_destroy": (_int, [_vp]),
 }
 
 _LIB = None

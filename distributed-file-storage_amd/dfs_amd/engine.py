@@ -557,6 +557,43 @@ class UploadPlan:
             pass
 
 
+class DownloadPlan:
+    """dfs_download_plan: the descriptor tables of one download shape built
+    once and kept in HBM (handleDownload with Base64 transport, SN:399-461 +
+    281-282); run() as download_device."""
+
+    def __init__(self, engine: FragmentEngine, spans: np.ndarray, nfiles: int, nfrag: int, file_len: np.ndarray,
+                 file_off: np.ndarray):
+        self.engine = engine
+        self.nfiles = nfiles
+        spans = np.ascontiguousarray(spans, dtype=np.uint64)
+        file_len = np.ascontiguousarray(file_len, dtype=np.uint64)
+        file_off = np.ascontiguousarray(file_off, dtype=np.uint64)
+        self._plan = ctypes.c_void_p()
+        check(lib().dfs_download_plan_create(engine.ctx, _ptr(spans), nfiles, nfrag, _ptr(file_len), _ptr(file_off),
+                                             ctypes.byref(self._plan)), "dfs_download_plan_create")
+
+    def run(self, d_b64: int, d_exp_frag: int, d_exp_file: int, d_out: int) -> np.ndarray:
+        status = np.zeros(max(self.nfiles, 1), dtype=np.int32)
+        rc = lib().dfs_download_plan_run(self.engine.ctx, self._plan, ctypes.c_void_p(d_b64 or None),
+                                        ctypes.c_void_p(d_exp_frag or None), ctypes.c_void_p(d_exp_file or None),
+                                        ctypes.c_void_p(d_out), _ptr(status))
+        if rc not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_DECODE, L.DFS_E_FRAG_MISMATCH, L.DFS_E_CORRUPT):
+            check(rc, "dfs_download_plan_run")
+        return status[:self.nfiles]
+
+    def close(self) -> None:
+        if self._plan:
+            lib().dfs_download_plan_destroy(self._plan)
+            self._plan = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def synth_fill(engine: FragmentEngine, d_dst: int, spans: np.ndarray, first_file: int, seed: int) -> None:
     spans = np.ascontiguousarray(spans, dtype=np.uint64)
     check(lib().dfs_synth_fill(engine.ctx, ctypes.c_void_p(d_dst), _ptr(spans), len(spans), first_file, seed),

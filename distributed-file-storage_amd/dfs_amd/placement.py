@@ -213,6 +213,105 @@ class Comm:
             pass
 
 
+def simulate_native(world: int, nfrag: int, table: np.ndarray, mode: str, src: Sequence[bytes],
+                    offline: Iterable[int] = ()) -> Tuple[List[bytes], np.ndarray]:
+    """dfs_place_simulate: the library's own runner (the code that issues the
+    RCCL calls) for every rank at once over host buffers and an in-process
+    stand-in for RCCL's group matching.  Returns (every rank's destination
+    buffer, (world, nfrag) fragment status); raises DfsError(DFS_E_COMM) when
+    sends and receives do not pair up."""
+    t = np.ascontiguousarray(table, dtype=np.uint64).reshape(world, nfrag)
+    sizes = [int(plan(world, r, nfrag, t, mode, offline)[1][nfrag]) for r in range(world)]
+    srcs = [np.frombuffer(bytes(s) or b"\0", dtype=np.uint8).copy() for s in src]
+    dsts = [np.zeros(max(n, 1), dtype=np.uint8) for n in sizes]
+    sp = (ctypes.c_void_p * world)(*[a.ctypes.data for a in srcs])
+    dp = (ctypes.c_void_p * world)(*[a.ctypes.data for a in dsts])
+    st = np.zeros((world, nfrag), dtype=np.int32)
+    _comm_error(lib().dfs_place_simulate(world, nfrag, t.ctypes.data, MODES[mode], offline_mask(offline), sp, dp,
+                                         st.ctypes.data), "dfs_place_simulate")
+    return [d[:n].tobytes() for d, n in zip(dsts, sizes)], st
+
+
+def replica_layout(world: int, rank: int, nfrag: int, file_lens: Sequence[Sequence[int]], align128: bool = False):
+    """dfs_replica_layout (pure host): what `rank` holds after a placement of
+    fragment-major uploads, file_lens[r] = rank r's file lengths.  Returns
+    (frags as a HELD_FRAG_DTYPE array in held order, (world, nfrag) Base64
+    group table, held_bytes, raw_bytes)."""
+    nfiles = np.array([len(x) for x in file_lens], dtype=np.uint32)
+    lens = np.array([int(v) for x in file_lens for v in x] or [0], dtype=np.uint64)
+    flags = L.DFS_LAYOUT_FRAG_MAJOR | (L.DFS_LAYOUT_ALIGN128 if align128 else 0)
+    n = ctypes.c_uint64(0)
+    table = np.zeros((world, nfrag), dtype=np.uint64)
+    held, raw = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(lib().dfs_replica_layout(world, rank, nfrag, nfiles.ctypes.data, lens.ctypes.data, flags, None,
+                                   ctypes.byref(n), table.ctypes.data, ctypes.byref(held), ctypes.byref(raw)),
+          "dfs_replica_layout")
+    frags = np.zeros(max(n.value, 1), dtype=L.HELD_FRAG_DTYPE)
+    check(lib().dfs_replica_layout(world, rank, nfrag, nfiles.ctypes.data, lens.ctypes.data, flags, frags.ctypes.data,
+                                   ctypes.byref(n), None, None, None), "dfs_replica_layout")
+    return frags[:n.value], table, held.value, raw.value
+
+
+class ReplicaPlan:
+    """dfs_replica_plan of one batch shape on one Comm: the replica receiver's
+    verify (SN:265-293 + 248-257) over the held buffer a placement filled."""
+
+    def __init__(self, comm: "Comm", nfrag: int, file_lens: Sequence[int], align128: bool = False):
+        self.comm = comm
+        lens = np.ascontiguousarray(file_lens, dtype=np.uint64)
+        nf = (ctypes.c_uint32 * 1)(len(lens))
+        lp = (ctypes.c_void_p * 1)(lens.ctypes.data if len(lens) else None)
+        out = (ctypes.c_void_p * 1)()
+        flags = L.DFS_LAYOUT_FRAG_MAJOR | (L.DFS_LAYOUT_ALIGN128 if align128 else 0)
+        _comm_error(lib().dfs_replica_plan_create(comm._arr(), 1, nfrag, nf, lp, flags, out), "dfs_replica_plan_create")
+        self._p = ctypes.c_void_p(out[0])
+        n, held, raw = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self.table = np.zeros((comm.world, nfrag), dtype=np.uint64)
+        check(lib().dfs_replica_plan_info(self._p, ctypes.byref(n), ctypes.byref(held), ctypes.byref(raw),
+                                          self.table.ctypes.data), "dfs_replica_plan_info")
+        self.nheld, self.held_bytes, self.raw_bytes = n.value, held.value, raw.value
+
+    def frags(self) -> np.ndarray:
+        out = np.zeros(max(self.nheld, 1), dtype=L.HELD_FRAG_DTYPE)
+        check(lib().dfs_replica_plan_frags(self._p, out.ctypes.data), "dfs_replica_plan_frags")
+        return out[:self.nheld]
+
+    def verify(self, d_frag_digest: int, d_held: int, d_raw: int, d_verdict: int, d_failed: int) -> None:
+        """Asynchronous on the comm's engine stream (dfs_replica_verify)."""
+        one = lambda v: (ctypes.c_void_p * 1)(v or None)  # noqa: E731
+        plans = (ctypes.c_void_p * 1)(self._p.value)
+        _comm_error(lib().dfs_replica_verify(self.comm._arr(), 1, plans, one(d_frag_digest), one(d_held), one(d_raw),
+                                             one(d_verdict), one(d_failed)), "dfs_replica_verify")
+
+    def exchange(self, d_frag_digest: int) -> None:
+        """Stage 1 (comm stream): this rank's digests to the holders."""
+        plans = (ctypes.c_void_p * 1)(self._p.value)
+        _comm_error(lib().dfs_replica_exchange(self.comm._arr(), 1, plans, (ctypes.c_void_p * 1)(d_frag_digest or None)),
+                    "dfs_replica_exchange")
+
+    def check(self, engine, d_held: int, d_raw: int, d_verdict: int, d_failed: int) -> None:
+        """Stage 2 (engine's stream, no communication): decode, hash, compare."""
+        c = ctypes.c_void_p
+        check(lib().dfs_replica_check(engine.ctx, self._p, c(d_held or None), c(d_raw or None), c(d_verdict or None),
+                                      c(d_failed or None)), "dfs_replica_check")
+
+    def report(self, d_failed: int) -> None:
+        """Stage 3 (comm stream): failures per uploader summed over the holders."""
+        _comm_error(lib().dfs_replica_report(self.comm._arr(), 1, (ctypes.c_void_p * 1)(d_failed or None)),
+                    "dfs_replica_report")
+
+    def close(self) -> None:
+        if self._p:
+            lib().dfs_replica_plan_destroy(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def frag_major_spans(file_lens: Sequence[int], nfrag: int):
     """(nfiles*nfrag, 2) uint64 spans of each (file, fragment) Base64 inside a
     fragment-major buffer ([fragment][file], the layout of a frag_major upload

@@ -248,6 +248,24 @@ int dfs_download_batch(dfs_ctx* ctx, const char* b64, const dfs_span* b64_msgs, 
                        const uint8_t* expected_file_digest, uint8_t* out, const uint64_t* file_off,
                        int32_t* status, uint32_t flags);
 
+/* ---- prepared download (descriptor build once, run many; device pointers) -- */
+/* dfs_download_batch rebuilds its descriptor tables (decode jobs, SHA lanes,
+ * group order) on the host on every call; for a batch shape that repeats —
+ * the same spans, file lengths and offsets, e.g. a node serving the same set
+ * of files, or a fixed-shape degraded read — a plan builds them once and
+ * keeps them in HBM.  Arguments as dfs_download_batch's; the mode (overlap /
+ * pipelined / serial) is the ctx's at creation.  nfiles >= 1. */
+typedef struct dfs_download_plan dfs_download_plan;
+int dfs_download_plan_create(dfs_ctx* ctx, const dfs_span* b64_msgs, uint32_t nfiles, uint32_t nfrag,
+                             const uint64_t* file_len, const uint64_t* file_off, dfs_download_plan** plan);
+/* d_b64, d_out (16-byte aligned) and the expected digests (may be NULL) are
+ * device memory; status (nfiles, host) as dfs_download_batch's.  The call
+ * synchronises (the verdict comes back); one run of a plan at a time. */
+int dfs_download_plan_run(dfs_ctx* ctx, dfs_download_plan* plan, const char* d_b64,
+                          const uint8_t* d_expected_frag_digest, const uint8_t* d_expected_file_digest, uint8_t* d_out,
+                          int32_t* status);
+int dfs_download_plan_destroy(dfs_download_plan* plan);
+
 /* ---- storeFragments wire codec, sender side (SN:195-205, 629-642) ------- */
 /* Length of the storeFragments body carrying fragments a and b of a file of
  * file_len bytes split into nfrag (buildFragmentsJson with two entries and
@@ -495,6 +513,98 @@ int dfs_place_star(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, cons
  * dfs_place_plan's.  Offline ranks neither serve nor request. */
 int dfs_fetch_degraded(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint64_t* table,
                        uint64_t offline_mask, const char* const* d_held, char* const* d_out, int32_t* frag_status);
+
+/* The same runner as dfs_place_ring / dfs_place_star / dfs_fetch_degraded,
+ * for all `nranks` ranks at once over HOST buffers and an in-process stand-in
+ * for RCCL's group semantics (no GPU, no RCCL call): per phase every rank's
+ * sends and receives are posted in the runner's order, then rank a's sends to
+ * b are paired with b's receives from a in posting order.  Unequal counts or
+ * sizes, a receive without a send, or a send that reads bytes written in the
+ * same group return DFS_E_COMM (dfs_comm_last_error names the pair).  It is
+ * how a schedule is checked before it meets hardware: src[r] / dst[r] are rank
+ * r's source groups (FETCH: its held buffer) and destination buffer,
+ * frag_status is nranks*nfrag (may be NULL). */
+int dfs_place_simulate(uint32_t nranks, uint32_t nfrag, const uint64_t* table, uint32_t mode, uint64_t offline_mask,
+                       const uint8_t* const* src, uint8_t* const* dst, int32_t* frag_status);
+
+/* ---- replica receiver over placed groups (SN:226-259, 265-293) ------------- */
+/* In the reference an upload succeeds only after every holder has
+ * Base64-decoded and hashed the pair it received (handleInternalStoreFragments,
+ * SN:281-282) and the uploader has compared those hashes with its own
+ * (sendFragmentsToNode, SN:248-257); a mismatch is "Replication failed"
+ * (SN:218-221).  After dfs_place_ring / dfs_place_star a rank holds, for every
+ * fragment f it hosts, group f of every rank.  dfs_replica_verify does the
+ * holders' half and the comparison for all of it:
+ *   1. every rank's fragment digests (what its upload computed) go to the
+ *      holders, fragment-major, 32 bytes per fragment, over the same comm and
+ *      with the placement's own schedule (so entry k of the table a holder
+ *      receives belongs to held fragment k);
+ *   2. each holder Base64-decodes every held fragment into d_raw (the bytes it
+ *      would store as <index>.frag, SN:284-285) and SHA-256s them;
+ *   3. verdict[k] = 0, DFS_E_DECODE (the decoder's IllegalArgumentException) or
+ *      DFS_E_FRAG_MISMATCH (digest or length differs from the uploader's);
+ *   4. failed[r] = fragments of uploader r that failed on ANY holder (summed
+ *      over the comm), so every uploader learns whether its upload replicated.
+ * Held fragments are numbered in held-buffer order: hosted fragment f
+ * ascending, then uploader rank, then that uploader's files in order
+ * (dfs_held_frag). */
+typedef struct dfs_held_frag {
+    uint32_t rank;     /* uploader                                         */
+    uint32_t file;     /* index among that uploader's files                */
+    uint32_t frag;     /* fragment number                                  */
+    uint32_t reserved;
+    uint64_t b64_off;  /* its Base64 in the held buffer                    */
+    uint64_t b64_len;
+    uint64_t raw_off;  /* its decoded bytes in d_raw (16-byte aligned)     */
+    uint64_t raw_len;
+} dfs_held_frag;
+/* Pure host: what rank `rank` of `nranks` holds after a placement of uploads
+ * whose Base64 is fragment-major (DFS_LAYOUT_FRAG_MAJOR, optionally
+ * DFS_LAYOUT_ALIGN128 in layout_flags).
+ *   nfiles[r]   files uploaded by rank r
+ *   file_len    every rank's file lengths, rank 0's first
+ *   frags       out, capacity *nfrags entries (NULL: count only); *nfrags = count
+ *   table       out (may be NULL): nranks*nfrag Base64 group bytes, what
+ *               dfs_place_sizes gathers and dfs_place_* take
+ *   held_bytes / raw_bytes  out (may be NULL): sizes of the held and raw buffers */
+int dfs_replica_layout(uint32_t nranks, uint32_t rank, uint32_t nfrag, const uint32_t* nfiles,
+                       const uint64_t* file_len, uint32_t layout_flags, dfs_held_frag* frags, uint64_t* nfrags,
+                       uint64_t* table, uint64_t* held_bytes, uint64_t* raw_bytes);
+typedef struct dfs_replica_plan dfs_replica_plan;
+/* Descriptors of one batch shape, built once and kept in HBM.  Every rank
+ * passes its own files' lengths; they are gathered over the comm (the call is
+ * a collective and synchronises).  plans: ncomms out. */
+int dfs_replica_plan_create(dfs_comm* const* comms, uint32_t ncomms, uint32_t nfrag, const uint32_t* nfiles,
+                            const uint64_t* const* file_len, uint32_t layout_flags, dfs_replica_plan** plans);
+/* nheld = held fragments; table (nranks*nfrag, may be NULL) as dfs_replica_layout's. */
+int dfs_replica_plan_info(const dfs_replica_plan* plan, uint64_t* nheld, uint64_t* held_bytes, uint64_t* raw_bytes,
+                          uint64_t* table);
+int dfs_replica_plan_frags(const dfs_replica_plan* plan, dfs_held_frag* frags);
+/* Asynchronous on each comm's ctx stream; a plan runs one verify at a time.
+ *   d_frag_digest  this rank's upload digests, [file][fragment] x 32 B
+ *                  (dfs_upload_plan_run's frag_digest)
+ *   d_held         the held buffer a placement filled
+ *   d_raw          out: raw_bytes of decoded fragments
+ *   d_verdict      out: nheld int32 (may be NULL)
+ *   d_failed       out: nranks uint32, identical on every rank afterwards */
+int dfs_replica_verify(dfs_comm* const* comms, uint32_t ncomms, dfs_replica_plan* const* plans,
+                       const uint8_t* const* d_frag_digest, const char* const* d_held, uint8_t* const* d_raw,
+                       int32_t* const* d_verdict, uint32_t* const* d_failed);
+/* The three stages of dfs_replica_verify on their own, for a pipeline that
+ * keeps the hashing off the communication stream (each asynchronous):
+ *   dfs_replica_exchange  comm streams: the digest tables to the holders;
+ *   dfs_replica_check     the stream of `ctx` (any ctx of the plan's device),
+ *                         no communication: decode, hash, compare; d_failed
+ *                         = this holder's own counts.  The caller orders it
+ *                         after the placement and the exchange (events);
+ *   dfs_replica_report    comm streams: d_failed summed over the holders
+ *                         (order it after dfs_replica_check). */
+int dfs_replica_exchange(dfs_comm* const* comms, uint32_t ncomms, dfs_replica_plan* const* plans,
+                         const uint8_t* const* d_frag_digest);
+int dfs_replica_check(dfs_ctx* ctx, dfs_replica_plan* plan, const char* d_held, uint8_t* d_raw, int32_t* d_verdict,
+                      uint32_t* d_failed);
+int dfs_replica_report(dfs_comm* const* comms, uint32_t ncomms, uint32_t* const* d_failed);
+int dfs_replica_plan_destroy(dfs_replica_plan* plan);
 
 /* ---- synthetic data (bench / tests) -------------------------------------- */
 /* Byte o of file (first_file_index + f) is byte o mod 8 (little endian) of

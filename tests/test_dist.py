@@ -76,6 +76,29 @@ def _worker(rank, world, port, nfrag, nfiles, offline, q):
                 assert dst[o:o + len(exp)].numpy().tobytes() == exp, (mode, rank, f)
             held[mode] = dst
         assert torch.equal(held["ring"], held["star"])
+        # replica receiver's verify (dfs_replica_verify): every rank's fragment
+        # digests travel fragment-major with the star schedule over 32 bytes
+        # per fragment; entry k of what a holder receives must be the digest of
+        # held fragment k of dfs_replica_layout, whose Base64 lies at b64_off
+        import hashlib
+        import oracle as O
+        lens_all = [[len(d) for d in _rank_files(r, nfiles)] for r in range(world)]
+        frags, rtable, held_bytes, _ = P.replica_layout(world, rank, nfrag, lens_all)
+        assert rtable.tolist() == table.tolist() and held_bytes == int(held["star"].numel())
+        mine = b"".join(hashlib.sha256(d[o:o + n]).digest() for f in range(nfrag) for d in files
+                        for o, n in [O.c_split(len(d), nfrag)[f]])
+        dsrc = torch.frombuffer(bytearray(mine), dtype=torch.uint8)
+        dtab = np.full((world, nfrag), 32 * nfiles, dtype=np.uint64)
+        dops, dlay, _ = P.plan(world, rank, nfrag, dtab, "star")
+        ddst = torch.zeros(int(dlay[nfrag]), dtype=torch.uint8)
+        P.run_plan_torch(dops, dsrc, ddst)
+        assert ddst.numel() == 32 * len(frags)
+        got, hb = ddst.numpy().tobytes(), held["star"].numpy().tobytes()
+        for k, x in enumerate(frags):
+            d = _rank_files(int(x["rank"]), nfiles)[int(x["file"])]
+            o, n = O.c_split(len(d), nfrag)[int(x["frag"])]
+            assert got[32 * k:32 * k + 32] == hashlib.sha256(d[o:o + n]).digest(), (rank, k)
+            assert hb[int(x["b64_off"]):int(x["b64_off"]) + int(x["b64_len"])] == O.c_b64_encode(d[o:o + n]), (rank, k)
         # degraded read: my own groups back from the live holders
         ops, lay, st = P.plan(world, rank, nfrag, table, "fetch", offline)
         out = torch.zeros(int(lay[nfrag]), dtype=torch.uint8)

@@ -819,6 +819,30 @@ def test_device_download_verdicts(engine, mode, monkeypatch):
         good = np.nonzero(want == 0)[0]
         o, f0 = out.view(nfiles, S), files[:nfiles * S].view(nfiles, S)
         assert torch.equal(o[torch.as_tensor(good)], f0[torch.as_tensor(good)])
+        # the same download through a prepared plan (tables built once, in HBM),
+        # run three times: same verdicts and bytes every time; then with the
+        # corruptions repaired it is clean
+        flen, foff = np.full(nfiles, S, np.uint64), np.arange(nfiles, dtype=np.uint64) * np.uint64(S)
+        dplan = dfs_amd.DownloadPlan(engine, msp, nfiles, nfrag, flen, foff)
+        for rep in range(3):
+            out.zero_()
+            st = dplan.run(b64.data_ptr(), frd.data_ptr(), fd.data_ptr(), out.data_ptr())
+            assert st.tolist() == want.tolist(), rep
+            assert torch.equal(out.view(nfiles, S)[torch.as_tensor(good)], f0[torch.as_tensor(good)]), rep
+        b64[int(msp[k, 0]) + 5] = ord("A")  # a valid char, but not the encoder's: the fragment digest differs
+        st = dplan.run(b64.data_ptr(), frd.data_ptr(), fd.data_ptr(), out.data_ptr())
+        want2 = want.copy()
+        want2[7] = dfs_amd.DFS_E_FRAG_MISMATCH
+        assert st.tolist() == want2.tolist()
+        assert dplan.run(b64.data_ptr(), 0, 0, out.data_ptr()).tolist() == \
+            [dfs_amd.DFS_E_MISSING if f == 9 else 0 for f in range(nfiles)]  # nothing to compare with
+        # an output that is not 16-byte aligned is not what the plan was tiled for
+        import ctypes as C
+        rc = dfs_amd.lib().dfs_download_plan_run(engine.ctx, dplan._plan, C.c_void_p(b64.data_ptr()), None, None,
+                                                 C.c_void_p(out.data_ptr() + 4), np.zeros(nfiles, np.int32).ctypes.data)
+        assert rc == dfs_amd.DFS_E_ARG
+        dplan.close()
+        assert engine.stats()["ovl_redo"] == 0
         plan.close()
     finally:
         if mode != "overlap":

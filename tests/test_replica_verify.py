@@ -1,0 +1,124 @@
+"""dfs_replica_verify on the GPU (one-rank communicator: every node on rank 0,
+so the held buffer is the upload's own Base64): the holders' decode + SHA-256
+of every held fragment (SN:281-282) and the comparison with the uploader's
+digests (SN:248-257), through the C ABI, against the oracle."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import dfs_amd
+import oracle as O
+from dfs_amd import _lib as L
+from dfs_amd import placement as P
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    with dfs_amd.FragmentEngine(0) as e:
+        yield e
+
+
+def _run(engine, lens, nfrag, align128, seed):
+    import torch
+    dev = torch.device("cuda", 0)
+    nfiles = len(lens)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    spans = np.stack([offs, np.array(lens, dtype=np.uint64)], axis=1)
+    total = int(sum(lens))
+    files = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
+    dfs_amd.synth_fill(engine, files.data_ptr(), spans, seed, O.SYNTH_SEED)
+    plan = dfs_amd.UploadPlan(engine, spans, nfrag, frag_major=True, align128=align128)
+    fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device=dev)
+    frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device=dev)
+    b64 = torch.zeros(max(plan.b64_total, 1), dtype=torch.uint8, device=dev)
+    plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
+    torch.cuda.synchronize()
+    comm = P.Comm(engine, P.unique_id(), 1, 0)
+    rp = P.ReplicaPlan(comm, nfrag, lens, align128)
+    return dict(torch=torch, dev=dev, files=files, plan=plan, frd=frd, b64=b64, comm=comm, rp=rp, nfiles=nfiles,
+                host=files.cpu().numpy(), offs=offs)
+
+
+@pytest.mark.parametrize("align128", [False, True])
+@pytest.mark.parametrize("shape", ["ragged", "uniform-large"])
+def test_replica_verify_single_rank(engine, align128, shape):
+    rng = np.random.default_rng(5 + align128)
+    nfrag = 5 if shape == "ragged" else 8
+    if shape == "ragged":
+        lens = [int(x) for x in rng.choice([0, 1, 4, 5, 63, 320, 4097, 20000, 65537], 300)]
+    else:
+        lens = [4096] * 9000  # 72,000 held fragments: the persistent SHA kernel
+    c = _run(engine, lens, nfrag, align128, 4200)
+    torch, dev, rp, comm = c["torch"], c["dev"], c["rp"], c["comm"]
+    try:
+        offs = c["plan"].b64_offsets()
+        grp = [int(offs[f]) for f in range(nfrag)] + [int(offs[-1])]
+        assert rp.table.tolist() == [[grp[f + 1] - grp[f] for f in range(nfrag)]]
+        assert rp.table.tolist() == comm.sizes([grp[f + 1] - grp[f] for f in range(nfrag)]).tolist()
+        assert rp.nheld == len(lens) * nfrag and rp.held_bytes == grp[-1]
+        held = torch.zeros(max(rp.held_bytes, 1), dtype=torch.uint8, device=dev)
+        comm.place("star", rp.table, c["b64"].data_ptr(), held.data_ptr())
+        raw = torch.zeros(rp.raw_bytes + 16, dtype=torch.uint8, device=dev)
+        verdict = torch.full((rp.nheld,), 99, dtype=torch.int32, device=dev)
+        failed = torch.full((1,), 99, dtype=torch.int32, device=dev)
+        print(f"replica verify {shape} align128={align128}: {rp.nheld} held fragments", flush=True)
+        rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
+        torch.cuda.synchronize()
+        assert int(failed[0]) == 0 and bool((verdict == 0).all())
+        frags = rp.frags()
+        rawh = raw.cpu().numpy()
+        for k in list(range(0, rp.nheld, max(1, rp.nheld // 97))) + [rp.nheld - 1]:
+            x = frags[k]
+            fo = int(c["offs"][int(x["file"])])
+            o, n = O.c_split(lens[int(x["file"])], nfrag)[int(x["frag"])]
+            assert int(x["raw_len"]) == n
+            assert rawh[int(x["raw_off"]):int(x["raw_off"]) + n].tobytes() == c["host"][fo + o:fo + o + n].tobytes(), k
+        # one held byte changed to another alphabet char: that fragment's digest differs (SN:250-257)
+        big = [k for k in range(rp.nheld) if int(frags[k]["b64_len"]) >= 8]
+        k1, k2 = big[len(big) // 3], big[2 * len(big) // 3]
+        p1 = int(frags[k1]["b64_off"]) + 5
+        old = int(held[p1])
+        held[p1] = ord("B") if old == ord("A") else ord("A")
+        rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
+        torch.cuda.synchronize()
+        v = verdict.cpu().numpy()
+        assert np.nonzero(v)[0].tolist() == [k1] and v[k1] == L.DFS_E_FRAG_MISMATCH and int(failed[0]) == 1
+        # and one byte outside the alphabet in another fragment: the decoder's IllegalArgumentException (SN:281)
+        held[int(frags[k2]["b64_off"]) + 2] = ord("!")
+        rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
+        torch.cuda.synchronize()
+        v = verdict.cpu().numpy()
+        assert sorted(np.nonzero(v)[0].tolist()) == sorted([k1, k2])
+        assert v[k1] == L.DFS_E_FRAG_MISMATCH and v[k2] == L.DFS_E_DECODE and int(failed[0]) == 2
+        # a wrong sender digest is a mismatch too; verdict may be NULL (counts only)
+        held[p1] = old
+        held[int(frags[k2]["b64_off"]) + 2] = ord("A")
+        frd2 = c["frd"].clone()
+        frd2[32 * 7 + 3] ^= 1  # file 1, fragment 2 of [file][fragment] (nfrag >= 5)
+        rp.verify(frd2.data_ptr(), held.data_ptr(), raw.data_ptr(), 0, failed.data_ptr())
+        torch.cuda.synchronize()
+        assert int(failed[0]) >= 1
+    finally:
+        rp.close()
+        comm.close()
+        c["plan"].close()
+
+
+def test_replica_verify_digest_is_the_oracles(engine):
+    """The digests compared are the oracle's: SHA-256(decode(encode(fragment)))
+    == SHA-256(fragment) per held fragment (the reference's own invariant)."""
+    lens = [28, 9506, 2154, 467]  # the reference's examples' sizes
+    c = _run(engine, lens, 5, False, 77)
+    try:
+        frd = c["frd"].cpu().numpy().reshape(len(lens), 5, 32)
+        for f, n in enumerate(lens):
+            d = c["host"][int(c["offs"][f]):int(c["offs"][f]) + n].tobytes()
+            for i, (o, ln) in enumerate(O.c_split(n, 5)):
+                assert frd[f, i].tobytes() == hashlib.sha256(d[o:o + ln]).digest()
+    finally:
+        c["rp"].close()
+        c["comm"].close()
+        c["plan"].close()
