@@ -51,6 +51,7 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
+constexpr uint64_t kMaxFile = 1ull << 37;  // the SHA lanes count 64-byte blocks in 32 bits
 
 // dfs_host_alloc buffers (base -> bytes, device-mapped base): a request is
 // direct only if each of its buffers lies inside one of them, so the copy
@@ -421,6 +422,10 @@ void worker_main(dfs_batcher* B, Worker* w) {
         }
         Timing tm;
         const int rc = batch.front()->kind == kUpload ? run_uploads(B, *w, batch, bs, tm) : run_downloads(B, *w, batch, bs, tm);
+        // A batch that failed part-way may have DMAs or kernels queued on the
+        // handlers' pinned buffers and on the staging: let them finish before
+        // any handler is told (it may free or reuse its buffers on return).
+        if (rc != DFS_OK) (void)wait_stream(*w);
         const auto t_done = Clock::now();
         // Results ready (or the batch failed); reuse the staging only after
         // every handler copied its output out.
@@ -596,6 +601,7 @@ int dfs_batcher_stats(dfs_batcher* B, dfs_batcher_stats_t* out) {
 int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t* file_digest, uint8_t* frag_digest,
                       char* b64, uint64_t b64_cap, uint64_t* b64_off) {
     if (!B || (len && !file) || !file_digest || !frag_digest || !b64_off) return DFS_E_ARG;
+    if (len >= kMaxFile) return DFS_E_ARG;  // refused here, to this caller only: a batch fails as a whole
     const uint32_t N = B->nfrag;
     dfs_span fr[64];
     if (dfs_split_plan(len, N, fr) != DFS_OK) return DFS_E_ARG;
@@ -620,10 +626,20 @@ int dfs_submit_download(dfs_batcher* B, const char* b64, const dfs_span* frags, 
     if (!B || !frags || (file_len && !out)) return DFS_E_ARG;
     Req r;
     r.kind = kDownload + (expected_frag_digest ? 2 : 0) + (expected_file_digest ? 1 : 0);
-    uint64_t need = 0;
+    // A request that could not run is refused here, to its caller only: inside
+    // a batch it would fail its neighbours' requests too.  The file cannot be
+    // longer than what its fragments' Base64 can decode to.
+    uint64_t need = 0, cap = 0;
     for (uint32_t k = 0; k < B->nfrag; ++k)
-        if (frags[k].len != DFS_SPAN_MISSING) need += frags[k].len;
+        if (frags[k].len != DFS_SPAN_MISSING) {
+            if (frags[k].len >= 2 * kMaxFile || frags[k].off >= (1ull << 62)) return DFS_E_ARG;
+            need += frags[k].len;
+            cap += dfs_b64_decoded_cap(frags[k].len);
+        }
     if (need && !b64) return DFS_E_ARG;
+    bool any_missing = false;
+    for (uint32_t k = 0; k < B->nfrag; ++k) any_missing = any_missing || frags[k].len == DFS_SPAN_MISSING;
+    if (file_len >= kMaxFile || (!any_missing && file_len > cap)) return DFS_E_ARG;
     r.text = b64;
     r.frags = frags;
     r.len = file_len;

@@ -80,6 +80,10 @@ struct dfs_ctx {
     uint32_t dec_prio = 1;       // decode waves at s_setprio 3 beside SHA (DFS_DEC_PRIO=0: 0)
     uint32_t dec_wgs = 1;        // decode workgroups per CU beside SHA (DFS_DEC_WGS)
     uint64_t ovl_redo = 0;       // overlap downloads whose SHA launch was redone (a wait timed out)
+    uint64_t wait_ticks = dfs::kShaWaitTicks;  // bound of an in-kernel group wait (DFS_SHA_WAIT_TICKS)
+    uint32_t wait_never = 0;     // test hook (DFS_SHA_WAIT_FORCE_TIMEOUT=1): the SHA lanes wait for one more
+                                 // workgroup than the decode / gather grid has and give up after 10 us, so
+                                 // every overlapped call takes the timeout + redo path; all kernels still exit
     hipEvent_t ev[2 * DFS_T_COUNT] = {};
     bool ev_used[DFS_T_COUNT] = {};
     hipEvent_t fork = nullptr, join = nullptr;  // SHA || Base64 on two streams
@@ -472,6 +476,12 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_OVL_DEC_WGS"))
         c->ovl_dec_wgs = static_cast<uint32_t>(std::max(1, std::min(4, std::atoi(w))));
     ovl_fit(c);
+    if (const char* w = std::getenv("DFS_SHA_WAIT_TICKS")) c->wait_ticks = std::max<uint64_t>(1, std::strtoull(w, nullptr, 10));
+    if (const char* w = std::getenv("DFS_SHA_WAIT_FORCE_TIMEOUT"))
+        if (std::atoi(w)) {
+            c->wait_never = 1;
+            c->wait_ticks = 1000;
+        }
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     if (const char* w = std::getenv("DFS_DEC_PRIO")) c->dec_prio = std::atoi(w) ? 1u : 0u;
@@ -1335,7 +1345,7 @@ int dfs_reassemble_verify(dfs_ctx* c, const uint8_t* const* src, const uint64_t*
         tm.end(DFS_T_GATHER, s);
         HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[0], 0));
         tm.begin(DFS_T_SHA, c->aux);
-        const dfs::ShaWait wt{d_queue + dfs::kShaWaitSlot, ah.grid, 1u, nfrag, 0u};
+        const dfs::ShaWait wt{d_queue + dfs::kShaWaitSlot, ah.grid + c->wait_never, 1u, nfrag, 0u, c->wait_ticks};
         HIPC(dfs::launch_sha256(d_out, c->buf[B_DESC].as<ShaDesc>(), static_cast<uint32_t>(sha.size()), nfiles, prio,
                                 d_dig, d_dig, d_queue, c->ovl_sha_wps, c->aux, nullptr, nullptr, &wt));
         tm.end(DFS_T_SHA, c->aux);
@@ -1605,7 +1615,8 @@ int run_dl(dfs_ctx* c, const DlTables& t, const DlDev& D, const char* d_in, uint
         // leave room for the decode waves, so the decode always progresses.
         HIPC(hipStreamWaitEvent(c->aux, c->pass_ev[0], 0));
         tm.begin(DFS_T_SHA, c->aux);
-        const dfs::ShaWait wt{d_queue + dfs::kShaWaitSlot, ah.grid, 1u, nfrag, static_cast<uint32_t>(nf)};
+        const dfs::ShaWait wt{d_queue + dfs::kShaWaitSlot, ah.grid + c->wait_never, 1u, nfrag, static_cast<uint32_t>(nf),
+                                c->wait_ticks};
         HIPC(dfs::launch_sha256(d_out, d_desc, t.nlanes[0], nout, t.prio[0], d_dig, d_dig, d_queue, c->ovl_sha_wps,
                                 c->aux, nullptr, nullptr, &wt));
         tm.end(DFS_T_SHA, c->aux);

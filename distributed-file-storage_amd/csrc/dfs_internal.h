@@ -139,12 +139,15 @@ struct BodyParse {
 // earlier launch on the stream the SHA launch waits for.  Fragment lanes
 // (digest slot out < nf) read group out % nfrag; fileId lanes (out >= nf,
 // whole files split SN:138-157 into nfrag fragments) wait at each fragment's
-// first block.  A wait is bounded: past kShaWaitTicks the lane goes on, sets
-// queue[2] and the host re-runs the SHA launch after the decode.
+// first block.  A wait is bounded: past `ticks` the lane goes on, sets
+// queue[2] (after which no lane of the launch waits again) and the host
+// re-runs the SHA launch after the decode.
 struct ShaWait {
     const uint32_t* done;
     uint32_t target, first, nfrag, nf;
+    uint64_t ticks;  // bound of one wait in s_memrealtime ticks (100 MHz)
 };
+constexpr uint64_t kShaWaitTicks = 200000000ull;  // 2 s
 constexpr uint32_t kShaWaitSlot = 8;  // done[g] = queue[kShaWaitSlot + g] (kShaQueueBytes)
 constexpr uint32_t kShaWaitMaxGroups = 48;
 // VGPRs per lane of the kernels that run in "ahead" mode beside the waiting

@@ -452,24 +452,27 @@ __device__ __forceinline__ uint32_t simd_key() {
 // ENC = the fused-Base64 instantiation (launched when the caller passes a
 // Base64 output; lanes flagged kShaB64 also write their message's Base64).
 constexpr uint32_t kStealSpins = 16;  // x s_sleep 127 (8,128 clocks each)
-constexpr uint64_t kShaWaitTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
 // Decode-ahead (ShaWait, dfs_internal.h): the active lanes of the wave wait
 // until fragment group `need` (per lane; ~0u = nothing to wait for) has been
 // published by every decode workgroup, then acquire at agent scope so the
 // loads that follow see the decoded bytes (the decode ran on other CUs / XCDs).
-// Bounded: on timeout queue[2] is set (the host re-runs the SHA launch after
+// Bounded (ShaWait::ticks of s_memrealtime): on timeout queue[2] is set (the host re-runs the SHA launch after
 // the decode) and the lane goes on, so the grid always drains.
 __device__ __forceinline__ void wait_group(const ShaWait& w, uint32_t need, uint32_t* __restrict__ queue) {
     const bool want = need != ~0u && need >= w.first;
     bool ok = !want || __hip_atomic_load(w.done + need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= w.target;
-    if (__ballot(!ok)) {
+    // Once any wave of the launch has timed out (queue[2]) the host will redo
+    // the whole launch after the decode: nobody waits again, so a launch that
+    // cannot run beside its decode stalls once, not once per item and group.
+    if (__ballot(!ok) && !__hip_atomic_load(queue + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
             __builtin_amdgcn_s_sleep(32);
             if (!ok) ok = __hip_atomic_load(w.done + need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= w.target;
             if (!__ballot(!ok)) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kShaWaitTicks) {
+            if (__hip_atomic_load(queue + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > w.ticks) {
                 atomicOr(queue + 2, 1u);
                 break;
             }

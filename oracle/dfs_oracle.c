@@ -361,6 +361,73 @@ double oracle_cpu_upload_bench(uint64_t seed, uint32_t nfiles, uint64_t flen, ui
     return j.err ? -2.0 : j.busy;
 }
 
+/* Checker for a whole synthetic batch (bench.py's verify leg and the GPU
+ * tests): for files [first, first + nfiles) of flen bytes, the fileId
+ * (SN:127), every fragment digest (SN:159) and the SHA-256 of every
+ * fragment's Base64 text (SN:636: a 32-byte stand-in for the text itself),
+ * one file per worker thread.  Returns 0, or < 0 on error. */
+typedef struct {
+    uint64_t seed, first; uint32_t nfiles; uint64_t flen; uint32_t nfrag; sha_fn sha;
+    uint8_t* fd; uint8_t* frd; uint8_t* b64d; uint32_t next; pthread_mutex_t mu; int err;
+} digest_job;
+
+static void* digest_worker(void* p) {
+    digest_job* j = (digest_job*)p;
+    const uint32_t N = j->nfrag;
+    uint8_t* file = (uint8_t*)malloc(j->flen ? j->flen : 1);
+    char* b64 = (char*)malloc(4 * ((j->flen / N + 3) / 3) + 16);
+    uint64_t* off = (uint64_t*)malloc(8 * N);
+    uint64_t* len = (uint64_t*)malloc(8 * N);
+    if (!file || !b64 || !off || !len) {
+        pthread_mutex_lock(&j->mu);
+        j->err = 1;
+        pthread_mutex_unlock(&j->mu);
+        goto out;
+    }
+    oracle_split(j->flen, N, off, len);
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        uint32_t f = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (f >= j->nfiles) break;
+        oracle_synth(j->seed, j->first + f, 0, j->flen, file);
+        j->sha(file, j->flen, j->fd + 32 * (uint64_t)f);
+        for (uint32_t i = 0; i < N; i++) {
+            const uint64_t k = (uint64_t)f * N + i;
+            j->sha(file + off[i], len[i], j->frd + 32 * k);
+            if (j->b64d) {
+                const uint64_t n = oracle_b64_encode(file + off[i], len[i], b64);
+                j->sha((const uint8_t*)b64, n, j->b64d + 32 * k);
+            }
+        }
+    }
+out:
+    free(file); free(b64); free(off); free(len);
+    return 0;
+}
+
+int oracle_synth_digests(uint64_t seed, uint64_t first, uint32_t nfiles, uint64_t flen, uint32_t nfrag, int threads,
+                         int use_openssl, uint8_t* fd, uint8_t* frd, uint8_t* b64d) {
+    sha_fn sha = oracle_sha256;
+    if (use_openssl) {
+        if (!g_ossl_sha256) {
+            void* h = dlopen("libcrypto.so.3", RTLD_NOW);
+            if (!h) h = dlopen("libcrypto.so", RTLD_NOW);
+            if (h) g_ossl_sha256 = (openssl_sha256_t)dlsym(h, "SHA256");
+        }
+        if (!g_ossl_sha256) return -1;
+        sha = sha_openssl;
+    }
+    if (!nfrag) return -3;
+    digest_job j = {seed, first, nfiles, flen, nfrag, sha, fd, frd, b64d, 0, PTHREAD_MUTEX_INITIALIZER, 0};
+    if (threads < 1) threads = 1;
+    pthread_t* t = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    for (int i = 0; i < threads; i++) pthread_create(&t[i], 0, digest_worker, &j);
+    for (int i = 0; i < threads; i++) pthread_join(t[i], 0);
+    free(t);
+    return j.err ? -2 : 0;
+}
+
 /* Download-side CPU baseline (bench.py cpu_baseline leg, download object):
  * per file, what the GPU download path computes — Base64-decode every
  * fragment (SN:281), SHA-256 it against the upload-time digest (SN:282,

@@ -80,6 +80,14 @@ void oracle_synth(uint64_t seed, uint64_t file_index, uint64_t start, uint64_t l
 double oracle_cpu_upload_bench(uint64_t seed, uint32_t nfiles, uint64_t file_len,
                                uint32_t nfrag, int threads, int use_openssl,
                                uint8_t* file_digest_out, uint8_t* frag_digest_out);
+/* Checker for a whole synthetic batch: files [first, first + nfiles) of
+ * file_len bytes (oracle_synth): file_digest (nfiles x 32, SN:127),
+ * frag_digest (nfiles x nfrag x 32, SN:159) and, if b64_digest is not NULL,
+ * the SHA-256 of every fragment's Base64 text (SN:636), one file per worker
+ * thread.  use_openssl as above (a second, independent SHA-256).  0 or < 0. */
+int oracle_synth_digests(uint64_t seed, uint64_t first, uint32_t nfiles, uint64_t file_len, uint32_t nfrag,
+                         int threads, int use_openssl, uint8_t* file_digest, uint8_t* frag_digest,
+                         uint8_t* b64_digest);
 /* Download-side CPU baseline: per file, Base64-decode each fragment (SN:281),
  * SHA-256 it against the upload digest (SN:282), ordered append (SN:448),
  * SHA-256 of the file against its fileId (SN:454).  Seconds of the slowest

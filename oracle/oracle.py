@@ -59,6 +59,9 @@ def lib() -> ctypes.CDLL:
     L.oracle_cpu_upload_bench.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                           ctypes.c_int, ctypes.c_int, u8p, u8p]
     L.oracle_cpu_upload_bench.restype = ctypes.c_double
+    L.oracle_synth_digests.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                       ctypes.c_uint32, ctypes.c_int, ctypes.c_int, u8p, u8p, u8p]
+    L.oracle_synth_digests.restype = ctypes.c_int
     L.oracle_cpu_download_bench.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_int, ctypes.c_int]
     L.oracle_cpu_download_bench.restype = ctypes.c_double
@@ -134,6 +137,27 @@ def cpu_upload_bench(nfiles: int, file_len: int, nfrag: int, threads: int, use_o
     secs = lib().oracle_cpu_upload_bench(seed, nfiles, file_len, nfrag, threads, int(use_openssl),
                                          fd.ctypes.data, frd.ctypes.data)
     return secs, fd, frd
+
+
+def synth_digests(first: int, nfiles: int, file_len: int, nfrag: int, threads: int, use_openssl: bool = True,
+                  with_b64: bool = True, seed: int = SYNTH_SEED):
+    """(file digests (n, 32), fragment digests (n, N, 32), SHA-256 of every
+    fragment's Base64 (n, N, 32) or None) of synthetic files [first, first+n):
+    the checker for a whole batch.  Falls back to the scalar SHA-256 when
+    libcrypto is not loadable."""
+    import numpy as np
+    fd = np.zeros((nfiles, 32), np.uint8)
+    frd = np.zeros((nfiles, nfrag, 32), np.uint8)
+    b64d = np.zeros((nfiles, nfrag, 32), np.uint8) if with_b64 else None
+    args = (seed, first, nfiles, file_len, nfrag, threads)
+    tail = (fd.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), frd.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+            b64d.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if with_b64 else None)
+    rc = lib().oracle_synth_digests(*args, int(use_openssl), *tail)
+    if rc == -1:
+        rc = lib().oracle_synth_digests(*args, 0, *tail)
+    if rc != 0:
+        raise RuntimeError(f"oracle_synth_digests failed ({rc})")
+    return fd, frd, b64d
 
 
 def cpu_download_bench(nfiles: int, file_len: int, nfrag: int, threads: int, use_openssl: bool,

@@ -634,7 +634,7 @@ def test_sha256_both_kernels_large_and_small_launches(engine):
     assert all(small[i].tobytes() == want[i] for i in range(5000))
 
 
-@pytest.mark.parametrize("mode", ["overlap", "pipelined", "serial"])
+@pytest.mark.parametrize("mode", ["overlap", "pipelined", "serial", "overlap-timeout"])
 def test_download_overlapped_large_batch(engine, mode, monkeypatch):
     """A download above dfs::kChainMaxLanes SHA lanes.  6,000 files (36,000
     lanes): every file rebuilt and verified, plus the failure statuses on a
@@ -648,8 +648,16 @@ def test_download_overlapped_large_batch(engine, mode, monkeypatch):
     group while the fileIds advance over group i - 1, their states in HBM
     between launches); DFS_DOWNLOAD_MODE=serial: the whole decode, then one
     SHA launch.  One unpadded fragment (valid for the JDK
-    decoder) shifts every later Base64 offset off dword alignment."""
-    if mode != "overlap":
+    decoder) shifts every later Base64 offset off dword alignment.
+    overlap-timeout: the same overlapped download with the in-kernel waits
+    forced to time out from the host (DFS_SHA_WAIT_FORCE_TIMEOUT: the lanes
+    wait for a count the decode never reaches and give up after 10 us; every
+    kernel still exits), so the SHA launch is redone after the decode: the
+    results must be the same and the redo counted."""
+    if mode == "overlap-timeout":
+        monkeypatch.setenv("DFS_SHA_WAIT_FORCE_TIMEOUT", "1")
+        engine = dfs_amd.FragmentEngine(0)
+    elif mode != "overlap":
         monkeypatch.setenv("DFS_DOWNLOAD_MODE", mode)
         engine = dfs_amd.FragmentEngine(0)
     import base64
@@ -680,7 +688,10 @@ def test_download_overlapped_large_batch(engine, mode, monkeypatch):
     texts[f][0] = texts[f][0].rstrip(b"=")
     try:
         res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
-        assert engine.stats()["ovl_redo"] == 0  # no decode-ahead wait timed out
+        if mode == "overlap-timeout":
+            assert engine.stats()["ovl_redo"] == 1  # the forced timeout was seen and the launch redone once
+        else:
+            assert engine.stats()["ovl_redo"] == 0  # no decode-ahead wait timed out
     finally:
         if mode != "overlap":
             engine.close()
@@ -717,7 +728,10 @@ def test_download_pipelined_many_fragments_small_files(engine, mode, monkeypatch
         file_h.append(hashlib.sha256(d).hexdigest())
     try:
         res = engine.download(texts, [len(d) for d in files], frag_h, file_h)
-        assert engine.stats()["ovl_redo"] == 0  # no decode-ahead wait timed out
+        if mode == "overlap-timeout":
+            assert engine.stats()["ovl_redo"] == 1  # the forced timeout was seen and the launch redone once
+        else:
+            assert engine.stats()["ovl_redo"] == 0  # no decode-ahead wait timed out
     finally:
         if mode != "overlap":
             engine.close()
@@ -726,7 +740,7 @@ def test_download_pipelined_many_fragments_small_files(engine, mode, monkeypatch
         assert body == files[f], f
 
 
-@pytest.mark.parametrize("mode", ["overlap", "serial"])
+@pytest.mark.parametrize("mode", ["overlap", "serial", "overlap-timeout"])
 def test_reassemble_large_batch_overlap(engine, mode, monkeypatch):
     """dfs_reassemble_verify above dfs::kChainMaxLanes files (SN:419-458, raw
     fragments): default (overlap) gathers fragment 0 of every file first, then
@@ -736,8 +750,12 @@ def test_reassemble_large_batch_overlap(engine, mode, monkeypatch):
     SN:455-458), a missing one (SN:443-446), empty and tiny files (fragments
     of 0 bytes, several fragments starting inside one block), and a batch
     whose fragment lengths are not the split's (a fetched fragment one byte
-    longer: the serial path, still verified)."""
-    if mode != "overlap":
+    longer: the serial path, still verified).  overlap-timeout: the in-kernel
+    waits forced to time out from the host, the fileId launch redone."""
+    if mode == "overlap-timeout":
+        monkeypatch.setenv("DFS_SHA_WAIT_FORCE_TIMEOUT", "1")
+        engine = dfs_amd.FragmentEngine(0)
+    elif mode != "overlap":
         monkeypatch.setenv("DFS_DOWNLOAD_MODE", mode)
         engine = dfs_amd.FragmentEngine(0)
     try:

@@ -265,6 +265,11 @@ int main(int argc, char** argv) {
     deadline = measure_from + dur(secs);
     go = true;
     std::this_thread::sleep_until(measure_from);
+    // the batcher's counters are cumulative since its creation: snapshot them
+    // where the measured window opens and report the differences, so that
+    // batches / requests / direct cover the window the throughput covers
+    dfs_batcher_stats_t st_warm{};
+    dfs_batcher_stats(B, &st_warm);
     unsigned long long u0, th0, u1, th1;
     cpu_stat(u0, th0);
     const auto t0 = Clock::now();
@@ -283,6 +288,15 @@ int main(int argc, char** argv) {
     auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, static_cast<size_t>(p * all.size()))]; };
     dfs_batcher_stats_t st{};
     dfs_batcher_stats(B, &st);
+    st.batches -= st_warm.batches;
+    st.requests -= st_warm.requests;
+    st.direct -= st_warm.direct;
+    st.queue_s -= st_warm.queue_s;
+    st.stage_in_s -= st_warm.stage_in_s;
+    st.device_s -= st_warm.device_s;
+    st.stage_out_s -= st_warm.stage_out_s;
+    st.enqueue_s -= st_warm.enqueue_s;
+    st.return_s -= st_warm.return_s;
     dfs_batcher_destroy(B);
     std::printf("{\"clients\": %d, \"kind\": \"%s\", \"requests\": %zu, \"wall_s\": %.4f, \"gbps\": %.4f, "
                 "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"cpu_s\": %.3f, \"throttled_s\": %.3f, \"cpu_threads_s\": {\"clients\": %.3f, \"workers\": %.3f, \"other\": %.3f}, \"client_cpu_us_per_req\": {\"in_submit\": %.1f, \"outside\": %.1f}, \"ok\": %s, \"file0_id\": \"%s\", \"file1_id\": \"%s\", "
