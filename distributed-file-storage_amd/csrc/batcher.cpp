@@ -93,7 +93,8 @@ struct BatchSync {
     double return_s = 0;         // handlers' results-ready -> return time
 };
 
-enum Kind { kUpload = 0, kDownload = 1 };  // download kinds: 1 + (exp_frag ? 2 : 0) + (exp_file ? 1 : 0)
+// download kinds: 1 + (exp_frag ? 2 : 0) + (exp_file ? 1 : 0); raw-fragment download: kReassemble
+enum Kind { kUpload = 0, kDownload = 1, kReassemble = 8 };
 
 struct Req {
     int kind = kUpload;
@@ -112,6 +113,10 @@ struct Req {
     const uint8_t* exp_frag = nullptr;
     const uint8_t* exp_file = nullptr;
     uint8_t* out = nullptr;
+    // raw-fragment download (handleDownload as the reference has it)
+    const uint8_t* const* raw = nullptr;  // the fragments, in index order
+    const uint64_t* raw_len = nullptr;
+    uint8_t* digest_out = nullptr;
     // hand-off
     Clock::time_point arrive;
     int phase = 0;
@@ -382,6 +387,48 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
     return DFS_OK;
 }
 
+// Raw-fragment downloads (handleDownload as the reference has it, SN:419-458:
+// getFragment returns raw bytes, SN:513-514).  The ordered append (SN:448) is
+// the handler's copy of its fragments, back to back, into the staging: the
+// staged bytes are the rebuilt file.  The device hashes every file of the
+// batch (SN:454); the handler compares with its fileId and takes the file
+// from the staging.  All requests are staged.
+int run_reassembles(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs, Timing& tm) {
+    (void)B;
+    const uint32_t n = static_cast<uint32_t>(batch.size());
+    std::vector<dfs_span> spans(n);
+    std::vector<uint64_t> in_off(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        in_off[i] = total;
+        spans[i] = dfs_span{total, batch[i]->len};
+        total += (batch[i]->len + 15) & ~15ull;
+    }
+    int rc = w.pin_in.grow(total + 16);
+    if (!rc) rc = w.pin_out.grow(32ull * n);
+    if (!rc) rc = w.d_in.grow(total + 16);
+    if (!rc) rc = w.d_dig.grow(32ull * n);
+    if (rc) return rc;
+    stage_in(B, batch, n, bs, w.pin_in.as<uint8_t>(), in_off, tm);
+    const auto t_dev = Clock::now();
+    if (total && hipMemcpyAsync(w.d_in.p, w.pin_in.p, total, hipMemcpyHostToDevice, w.stream) != hipSuccess)
+        return DFS_E_HIP;
+    rc = dfs_sha256_batch(w.ctx, w.d_in.as<uint8_t>(), spans.data(), n, w.d_dig.as<uint8_t>(), DFS_DEVICE_PTRS);
+    if (rc) return rc;
+    if (hipMemcpyAsync(w.pin_out.p, w.d_dig.p, 32ull * n, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
+        return DFS_E_HIP;
+    if (!wait_stream(w)) return DFS_E_HIP;
+    tm.device = since(t_dev);
+    for (uint32_t i = 0; i < n; ++i) {
+        Req* r = batch[i];
+        const uint8_t* d = w.pin_out.as<uint8_t>() + 32ull * i;
+        if (r->digest_out) std::memcpy(r->digest_out, d, 32);
+        r->status = r->exp_file && std::memcmp(d, r->exp_file, 32) != 0 ? DFS_E_CORRUPT : DFS_OK;  // SN:455-458
+        r->out_src = w.pin_in.as<uint8_t>() + in_off[i];  // the rebuilt file, where the handler assembled it
+    }
+    return DFS_OK;
+}
+
 void worker_main(dfs_batcher* B, Worker* w) {
     (void)pthread_setname_np(pthread_self(), "dfs-batch");  // per-thread CPU accounting (tools/batcher_load)
     (void)hipSetDevice(B->device);
@@ -421,7 +468,10 @@ void worker_main(dfs_batcher* B, Worker* w) {
             if (!B->q.empty()) B->cv_work.notify_one();
         }
         Timing tm;
-        const int rc = batch.front()->kind == kUpload ? run_uploads(B, *w, batch, bs, tm) : run_downloads(B, *w, batch, bs, tm);
+        const int kind0 = batch.front()->kind;
+        const int rc = kind0 == kUpload ? run_uploads(B, *w, batch, bs, tm)
+                       : kind0 == kReassemble ? run_reassembles(B, *w, batch, bs, tm)
+                                              : run_downloads(B, *w, batch, bs, tm);
         // A batch that failed part-way may have DMAs or kernels queued on the
         // handlers' pinned buffers and on the staging: let them finish before
         // any handler is told (it may free or reuse its buffers on return).
@@ -469,6 +519,12 @@ int submit(dfs_batcher* B, Req& r) {
         lk.unlock();
         if (r.kind == kUpload) {
             if (r.len) std::memcpy(r.in_dst, r.file, r.len);
+        } else if (r.kind == kReassemble) {  // full.write(fragData) in index order, SN:448
+            uint8_t* d = r.in_dst;
+            for (uint32_t k = 0; k < B->nfrag; ++k) {
+                if (r.raw_len[k]) std::memcpy(d, r.raw[k], r.raw_len[k]);
+                d += r.raw_len[k];
+            }
         } else {  // the fragments' Base64 back to back (run_downloads rebases the spans)
             uint8_t* d = r.in_dst;
             for (uint32_t k = 0; k < B->nfrag; ++k) {
@@ -618,6 +674,27 @@ int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t
     r.b64 = b64;
     r.b64_off = b64_off;
     r.direct = in_pinned(file, len) && in_pinned(b64, r.out_bytes);
+    return submit(B, r);
+}
+
+int dfs_submit_reassemble(dfs_batcher* B, const uint8_t* const* frags, const uint64_t* frag_len,
+                          const uint8_t* expected_file_digest, uint8_t* out, uint8_t* file_digest_out) {
+    if (!B || !frags || !frag_len) return DFS_E_ARG;
+    uint64_t len = 0;
+    for (uint32_t k = 0; k < B->nfrag; ++k) {
+        if (!frags[k] && frag_len[k]) return DFS_E_MISSING;  // "Could not retrieve fragment i", SN:443-446: nothing is hashed
+        if (frag_len[k] >= kMaxFile) return DFS_E_ARG;
+        len += frag_len[k];
+    }
+    if (len >= kMaxFile || (len && !out)) return DFS_E_ARG;
+    Req r;
+    r.kind = kReassemble;
+    r.raw = frags;
+    r.raw_len = frag_len;
+    r.len = r.need = r.out_bytes = len;
+    r.exp_file = expected_file_digest;
+    r.out = out;
+    r.digest_out = file_digest_out;
     return submit(B, r);
 }
 

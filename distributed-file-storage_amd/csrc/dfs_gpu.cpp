@@ -54,7 +54,7 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
-enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_STATUS, B_OUTLEN, B_QUEUE, B_COPY, B_COUNT };
+enum BufId { B_DATA_IN, B_DATA_OUT, B_DIG0, B_DIG1, B_DESC, B_JOBS, B_JOBS2, B_JOBS3, B_STATUS, B_OUTLEN, B_QUEUE, B_COPY, B_COUNT };
 
 }  // namespace
 
@@ -68,7 +68,8 @@ struct dfs_ctx {
     bool profiling = false;
     int sha_wps = 4;             // SHA waves per SIMD (DFS_SHA_WPS overrides)
     int sha_wps_beside = 3;      // ... when the Base64 kernel runs beside it (4 x 116 VGPRs leave no room)
-    int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels (DFS_UPLOAD_MODE)
+    int upload_mode = 1;         // 0 fused Base64 in the SHA lanes, 1 SHA || Base64 kernels, 2 hybrid: the fragment
+                                 // lanes write their own Base64 and the encode kernel only the twins' (DFS_UPLOAD_MODE)
     int download_mode = 2;       // 2 decode-ahead (one SHA launch waits per fragment group), 0 pipelined passes,
                                  // 1 decode then SHA (DFS_DOWNLOAD_MODE=overlap|pipelined|serial)
     int ovl_sha_wps = 3;         // overlap: SHA waves per SIMD (DFS_OVL_SHA_WPS) ...
@@ -166,6 +167,9 @@ struct dfs_upload_plan {
     StreamJob* d_enc = nullptr;
     uint32_t n_enc = 0;
     uint64_t enc_tiles = 0;
+    StreamJob* d_enc_twin = nullptr;  // the encode jobs of the fragments that ride as twins (hybrid mode)
+    uint32_t n_enc_twin = 0;
+    uint64_t enc_twin_tiles = 0;
     std::vector<uint64_t> b64_off;
     uint64_t b64_total = 0;
 };
@@ -469,7 +473,8 @@ int dfs_open(dfs_ctx** out, int device) {
     if (!c) return DFS_E_NOMEM;
     c->device = device;
     if (const char* w = std::getenv("DFS_SHA_WPS")) c->sha_wps = c->sha_wps_beside = std::max(1, std::min(8, std::atoi(w)));
-    if (const char* w = std::getenv("DFS_UPLOAD_MODE")) c->upload_mode = std::strcmp(w, "fused") == 0 ? 0 : 1;
+    if (const char* w = std::getenv("DFS_UPLOAD_MODE"))
+        c->upload_mode = std::strcmp(w, "fused") == 0 ? 0 : (std::strcmp(w, "hybrid") == 0 ? 2 : 1);
     if (const char* w = std::getenv("DFS_DOWNLOAD_MODE"))
         c->download_mode = std::strcmp(w, "serial") == 0 ? 1 : (std::strcmp(w, "pipelined") == 0 ? 0 : 2);
     if (const char* w = std::getenv("DFS_OVL_SHA_WPS")) c->ovl_sha_wps = std::max(1, std::min(3, std::atoi(w)));
@@ -900,10 +905,10 @@ namespace {
 // fragments alone), encode jobs, Base64 layout.
 struct HostPlan {
     std::vector<ShaDesc> all, frag;  // all = n_all lanes (fileIds + fragments) then their twins
-    std::vector<StreamJob> enc;
+    std::vector<StreamJob> enc, enc_twin;  // every fragment's encode job; those of the twins alone
     std::vector<uint64_t> b64_off;
     uint32_t prio_all = 0, prio_frag = 0, n_all = 0;
-    uint64_t enc_tiles = 0, total = 0;
+    uint64_t enc_tiles = 0, enc_twin_tiles = 0, total = 0;
     bool twins = false;
 };
 
@@ -991,6 +996,23 @@ int build_host_plan(const dfs_span* files, uint32_t nfiles, uint32_t nfrag, uint
     h.prio_all = sort_lanes(lanes);  // twins stay behind the lanes, unsorted
     std::copy(lanes.begin(), lanes.end(), h.all.begin());
     h.prio_frag = sort_lanes(h.frag);
+    // Hybrid upload: the fragment lanes write their own Base64 in the SHA pass
+    // (kShaB64) and the encode kernel covers only the fragments hashed as
+    // twins inside their fileId lane (the lane holds their blocks in registers
+    // once, for two states; encoding there as well would put the Base64 on
+    // the critical chain).
+    h.enc_twin.clear();
+    std::vector<uint64_t> titems;
+    if (h.twins) {
+        std::vector<uint8_t> is_twin(nf, 0);
+        for (size_t i = h.n_all; i < h.all.size(); ++i) is_twin[h.all[i].out - nfiles] = 1;
+        for (size_t q = 0; q + 0 < h.enc.size(); ++q)
+            if (is_twin[h.enc[q].id]) {
+                h.enc_twin.push_back(h.enc[q]);
+                titems.push_back(items[q]);
+            }
+    }
+    h.enc_twin_tiles = finish_jobs(h.enc_twin, titems, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
     h.enc_tiles = finish_jobs(h.enc, items, static_cast<uint64_t>(dfs::kEncPer) * dfs::kStreamBlock);
     return DFS_OK;
 }
@@ -1006,6 +1028,8 @@ void fill_plan_header(dfs_upload_plan* p, const HostPlan& h, int device, uint32_
     p->n_frag_only = static_cast<uint32_t>(h.frag.size());
     p->n_enc = static_cast<uint32_t>(h.enc.size() - 1);  // minus the sentinel
     p->enc_tiles = h.enc_tiles;
+    p->n_enc_twin = static_cast<uint32_t>(h.enc_twin.size() - 1);
+    p->enc_twin_tiles = h.enc_twin_tiles;
     p->b64_total = h.total;
 }
 
@@ -1017,7 +1041,9 @@ int scratch_plan(dfs_ctx* c, const HostPlan& h, uint32_t nfiles, uint32_t nfrag,
     if (int rc = put(c, B_DESC, h.all.data(), h.all.size() * sizeof(ShaDesc), s)) return rc;
     if (int rc = put(c, B_JOBS2, h.frag.data(), h.frag.size() * sizeof(ShaDesc), s)) return rc;
     if (int rc = put(c, B_JOBS, h.enc.data(), h.enc.size() * sizeof(StreamJob), s)) return rc;
+    if (int rc = put(c, B_JOBS3, h.enc_twin.data(), h.enc_twin.size() * sizeof(StreamJob), s)) return rc;
     HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    p.d_enc_twin = c->buf[B_JOBS3].as<StreamJob>();
     p.d_all = c->buf[B_DESC].as<ShaDesc>();
     p.d_frag = c->buf[B_JOBS2].as<ShaDesc>();
     p.d_enc = c->buf[B_JOBS].as<StreamJob>();
@@ -1046,6 +1072,9 @@ int dfs_upload_plan_create(dfs_ctx* c, const dfs_span* files, uint32_t nfiles, u
     if (e == hipSuccess) e = hipMalloc(&p->d_all, std::max<size_t>(h.all.size(), 1) * sizeof(ShaDesc));
     if (e == hipSuccess) e = hipMalloc(&p->d_frag, std::max<size_t>(h.frag.size(), 1) * sizeof(ShaDesc));
     if (e == hipSuccess) e = hipMalloc(&p->d_enc, h.enc.size() * sizeof(StreamJob));
+    if (e == hipSuccess) e = hipMalloc(&p->d_enc_twin, h.enc_twin.size() * sizeof(StreamJob));
+    if (e == hipSuccess)
+        e = hipMemcpy(p->d_enc_twin, h.enc_twin.data(), h.enc_twin.size() * sizeof(StreamJob), hipMemcpyHostToDevice);
     if (e == hipSuccess && !h.all.empty())
         e = hipMemcpy(p->d_all, h.all.data(), h.all.size() * sizeof(ShaDesc), hipMemcpyHostToDevice);
     if (e == hipSuccess && !h.frag.empty())
@@ -1074,6 +1103,7 @@ int dfs_upload_plan_destroy(dfs_upload_plan* p) {
     if (p->d_all) (void)hipFree(p->d_all);
     if (p->d_frag) (void)hipFree(p->d_frag);
     if (p->d_enc) (void)hipFree(p->d_enc);
+    if (p->d_enc_twin) (void)hipFree(p->d_enc_twin);
     delete p;
     return DFS_OK;
 }
@@ -1084,7 +1114,13 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     const bool do_fileid = !(flags & DFS_NO_FILEID);
     const bool do_b64 = !(flags & DFS_NO_B64) && p->n_enc;
     const bool serial = flags & DFS_SERIAL;
-    const bool fused = do_b64 && c->upload_mode == 0 && !serial && !p->twins;  // twins: plain kernel only
+    // Fused (DFS_UPLOAD_MODE=fused, plans without twins): the fragment lanes
+    // write every fragment's Base64.  Hybrid (DFS_UPLOAD_MODE=hybrid): the same
+    // kernel on a plan with twins; the fragments that ride in their fileId
+    // lane are encoded by the encode kernel beside it (a fifth of the bytes
+    // for 1 MiB / N = 5; every fragment when all of them are twins).
+    const bool hybrid = do_b64 && c->upload_mode == 2 && !serial;
+    const bool fused = do_b64 && !serial && (hybrid || (c->upload_mode == 0 && !p->twins));
     if (!d_frd || (do_fileid && !d_fd) || (do_b64 && !d_b64)) return DFS_E_ARG;
     if (do_b64 && (reinterpret_cast<uintptr_t>(d_b64) & 3u)) return DFS_E_ARG;
     hipStream_t s = c->stream();
@@ -1102,7 +1138,12 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     if (!serial && !c->aux) HIPC(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
     hipStream_t sb = serial ? s : c->aux;
     Timer tm(c);
-    const bool two = do_b64 && !fused;  // separate Base64 encode kernel
+    // separate Base64 encode kernel: every fragment, or (hybrid) the twins'
+    const bool twin_enc = fused && hybrid && do_fileid && p->twins && p->n_enc_twin;
+    const bool two = do_b64 && (!fused || twin_enc);
+    const StreamJob* enc_jobs = twin_enc ? p->d_enc_twin : p->d_enc;
+    const uint32_t enc_n = twin_enc ? p->n_enc_twin : p->n_enc;
+    const uint64_t enc_tiles = twin_enc ? p->enc_twin_tiles : p->enc_tiles;
     const int wps = two && !serial ? c->sha_wps_beside : c->sha_wps;
     tm.begin(DFS_T_TOTAL, s);
     if (two && !serial) {  // fork: Base64 on the aux stream beside SHA
@@ -1122,7 +1163,7 @@ int run_plan_locked(dfs_ctx* c, dfs_upload_plan* p, const uint8_t* d_files, uint
     tm.end(DFS_T_SHA, s);
     if (two) {
         tm.begin(DFS_T_B64ENC, sb);
-        HIPC(dfs::launch_b64_encode(d_files, p->d_enc, p->n_enc, p->enc_tiles, d_b64,
+        HIPC(dfs::launch_b64_encode(d_files, enc_jobs, enc_n, enc_tiles, d_b64,
                                     serial ? 8u : static_cast<uint32_t>(c->b64_wgs), sb, c->b64_prio));
         tm.end(DFS_T_B64ENC, sb);
         if (!serial) {  // join

@@ -450,7 +450,9 @@ __device__ __forceinline__ uint32_t simd_key() {
 // queue[0] = long counter, queue[1] = short counter, queue[64 + key] = SIMD
 // token counters; all zeroed by the launcher before each launch.
 // ENC = the fused-Base64 instantiation (launched when the caller passes a
-// Base64 output; lanes flagged kShaB64 also write their message's Base64).
+// Base64 output): lanes flagged kShaB64 also write their message's Base64;
+// every other lane of the launch (fileId lanes, twins included) hashes as in
+// the plain instantiation.
 constexpr uint32_t kStealSpins = 16;  // x s_sleep 127 (8,128 clocks each)
 
 // Decode-ahead (ShaWait, dfs_internal.h): the active lanes of the wave wait
@@ -544,8 +546,11 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
         // the loop state on every exit edge (192 VGPRs, 2 waves/SIMD); lanes
         // past their own length run the body on a clamped block and park
         // their state in LDS.
+        // Only the lanes that encode (kShaB64) run that loop; the others
+        // (fileId lanes, with or without twins) take the plain path below.
         const uint32_t kmax =
-            ENC ? __builtin_amdgcn_readfirstlane(wave_max(gid < n ? static_cast<uint32_t>(descs[gid].len >> 6) : 0u))
+            ENC ? __builtin_amdgcn_readfirstlane(wave_max(
+                      gid < n && (descs[gid].flags & kShaB64) ? static_cast<uint32_t>(descs[gid].len >> 6) : 0u))
                 : 0u;
         if (gid < n) {
             const Msg m = msg_setup(base, descs[gid]);
@@ -558,8 +563,8 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
             } else {
                 init_state(st);
             }
-            if (ENC) {
-                const bool enc = (m.flags & kShaB64) != 0u;
+            if (ENC && (m.flags & kShaB64) != 0u) {
+                const bool enc = true;
                 char* bdst = b64 + descs[gid].b64;
                 if (kmax) {
                     // C holds block k, N receives block k+1 (clamped) while C

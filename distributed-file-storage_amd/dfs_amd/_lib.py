@@ -128,6 +128,7 @@ SIGNATURES = {
     "dfs_host_free": (_int, [_vp]),
     "dfs_submit_upload": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
     "dfs_submit_download": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "dfs_submit_reassemble": (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "dfs_comm_unique_id": (_int, [_vp]),
     "dfs_comm_init_rank": (_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_vp)]),
     "dfs_comm_init_all": (_int, [_vp, _u32, _vp]),

@@ -99,6 +99,28 @@ class Batcher:
             check(st, "dfs_submit_download")
         return st, (out[:file_len].tobytes() if st == 0 else None)
 
+    def reassemble(self, frags: Sequence[Optional[bytes]], file_digest: Optional[bytes]
+                   ) -> Tuple[int, Optional[bytes], Optional[bytes]]:
+        """Raw-fragment download of one file (handleDownload as the reference
+        has it, SN:419-458): (status, rebuilt bytes or None, SHA-256 of the
+        rebuilt bytes or None)."""
+        assert len(frags) == self.nfrag
+        keep = [np.frombuffer(f, np.uint8).copy() if f else None for f in frags]
+        ptrs = (ctypes.c_void_p * self.nfrag)(*[a.ctypes.data if a is not None and a.size else None for a in keep])
+        lens = (ctypes.c_uint64 * self.nfrag)(*[1 if f is None else len(f) for f in frags])  # None: a missing fragment
+        for i, f in enumerate(frags):
+            if f is not None and not f:
+                lens[i] = 0
+        total = sum(len(f) for f in frags if f is not None)
+        out = np.zeros(max(total, 1), np.uint8)
+        dig = np.zeros(32, np.uint8)
+        ei = np.frombuffer(file_digest, np.uint8) if file_digest is not None else None
+        st = lib().dfs_submit_reassemble(self._b, ptrs, lens, ei.ctypes.data if ei is not None else None,
+                                         out.ctypes.data, dig.ctypes.data)
+        if st not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_CORRUPT):
+            check(st, "dfs_submit_reassemble")
+        return st, (out[:total].tobytes() if st == 0 else None), (dig.tobytes() if st != L.DFS_E_MISSING else None)
+
     def stats(self) -> dict:
         st = L.dfs_batcher_stats_t()
         check(lib().dfs_batcher_stats(self._b, ctypes.byref(st)), "dfs_batcher_stats")

@@ -220,6 +220,55 @@ public:
 
     dfs_ctx* raw() { return ctx_; }
 
+    // ---- the same two handler operations through a process-wide request
+    // batcher (dfs_batcher): StorageNode runs one thread per connection
+    // (SN:28-31), each handling ONE file; concurrent handlers' files run as
+    // one launch.  Results are identical to upload() / reassembleAndVerify().
+    static std::pair<std::string, std::vector<Fragment>> upload(dfs_batcher* b, const Bytes& file, int parts) {
+        std::vector<uint8_t> fd(32), frd(32ull * parts);
+        std::vector<uint64_t> off(parts + 1);
+        std::vector<dfs_span> split(parts);
+        check(dfs_split_plan(file.size(), parts, split.data()), "split");
+        uint64_t cap = 0;
+        for (auto& s : split) cap += dfs_b64_encoded_len(s.len);
+        std::string b64(cap, '\0');
+        check(dfs_submit_upload(b, file.empty() ? nullptr : file.data(), file.size(), fd.data(), frd.data(),
+                                cap ? &b64[0] : nullptr, cap, off.data()),
+              "handleUpload");
+        std::vector<Fragment> frags;
+        for (int i = 0; i < parts; ++i) {
+            Fragment f;
+            f.index = i;
+            f.data.assign(file.begin() + split[i].off, file.begin() + split[i].off + split[i].len);
+            f.hash = hex(frd.data() + 32 * i);
+            f.b64 = b64.substr(off[i], off[i + 1] - off[i]);
+            frags.push_back(std::move(f));
+        }
+        return {hex(fd.data()), std::move(frags)};
+    }
+
+    static Bytes reassembleAndVerify(dfs_batcher* b, const std::string& fileId,
+                                     const std::vector<std::optional<Bytes>>& frags) {
+        const uint32_t n = static_cast<uint32_t>(frags.size());
+        std::vector<const uint8_t*> src(n);
+        std::vector<uint64_t> len(n);
+        uint64_t total = 0;
+        static const uint8_t empty = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (!frags[i]) throw DownloadError(DFS_E_MISSING, "Could not retrieve fragment " + std::to_string(i));
+            src[i] = frags[i]->empty() ? &empty : frags[i]->data();
+            len[i] = frags[i]->size();
+            total += len[i];
+        }
+        Bytes out(total ? total : 1);
+        const Bytes want = unhex(fileId);
+        const int rc = dfs_submit_reassemble(b, src.data(), len.data(), want.data(), out.data(), nullptr);
+        if (rc == DFS_E_CORRUPT) throw DownloadError(DFS_E_CORRUPT, "File corrupted");
+        check(rc, "handleDownload");
+        out.resize(total);
+        return out;
+    }
+
 private:
     static void check(int rc, const char* where) {
         if (rc != DFS_OK) throw std::runtime_error(std::string(where) + ": " + dfs_strerror(rc));

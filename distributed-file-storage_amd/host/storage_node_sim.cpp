@@ -17,18 +17,31 @@
 // The data directory is $DFS_SIM_DATA (kept), else a fresh /tmp directory
 // removed at exit.
 //
-// usage: storage_node_sim <file>...   (prints the log to stdout; exit 0 = all
-//        downloads verified bit-exact)
+// Handlers run as in the reference: one thread per connection (SN:28-31), one
+// file per request.  The uploads of all files run concurrently on their own
+// threads, then (node 3 down) each node's downloads do; every handler goes
+// through the process-wide request batcher (dfs_submit_upload for SN:118-171,
+// dfs_submit_reassemble for SN:419-458), which runs the concurrent requests as
+// one launch.  A handler writes its log lines to its own buffer; the buffers
+// are printed in request order, so the log is the same as a serial run's.
+// --serial: the same replay with one handler at a time through the per-call
+// ABI (dfs_upload_batch / dfs_reassemble_verify).
+//
+// usage: storage_node_sim [--serial] <file>...   (prints the log to stdout;
+//        exit 0 = all downloads verified bit-exact)
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <filesystem>
 #include <fstream>
 #include <iterator>
 #include <map>
+#include <mutex>
 #include <optional>
 #include <set>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fragment_engine.hpp"
@@ -37,6 +50,20 @@ namespace {
 
 constexpr int TOTAL_NODES = 5;  // SN:15
 namespace fs = std::filesystem;
+
+// One handler's log lines (System.out.printf in the reference), printed by
+// the main thread in request order.
+struct Log {
+    std::string text;
+    void printf(const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        const int n = std::vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        text.append(buf, n < 0 ? 0 : std::min<size_t>(static_cast<size_t>(n), sizeof buf - 1));
+    }
+};
 
 std::string basename_of(const std::string& p) {
     const size_t s = p.find_last_of('/');
@@ -121,8 +148,19 @@ struct Node {
 
 struct Cluster {
     dfs::FragmentEngine eng;
+    dfs_batcher* batcher = nullptr;  // nullptr: --serial, the per-call ABI
+    std::mutex mu;                   // the manifests (handlers run concurrently)
     std::vector<Node> nodes;
-    explicit Cluster(const std::string& data) {
+    ~Cluster() {
+        if (batcher) dfs_batcher_destroy(batcher);
+    }
+    explicit Cluster(const std::string& data, bool threaded) {
+        if (threaded) {
+            dfs_batcher_opts o{};
+            o.max_wait_us = 2000;
+            const int rc = dfs_batcher_create(0, TOTAL_NODES, &o, &batcher);
+            if (rc != DFS_OK) throw std::runtime_error(std::string("dfs_batcher_create: ") + dfs_strerror(rc));
+        }
         for (int i = 1; i <= TOTAL_NODES; ++i) {
             nodes.emplace_back();
             nodes.back().id = i;
@@ -157,18 +195,18 @@ struct Cluster {
     }
 
     // handleUpload on node u (SN:118-189).
-    std::string upload(int u, const std::string& name, const dfs::Bytes& file) {
-        std::printf("[%d] Received upload: %zu bytes\n", u, file.size());
-        auto up = eng.upload(file, TOTAL_NODES);
+    std::string upload(int u, const std::string& name, const dfs::Bytes& file, Log& out) {
+        out.printf("[%d] Received upload: %zu bytes\n", u, file.size());
+        auto up = batcher ? dfs::FragmentEngine::upload(batcher, file, TOTAL_NODES) : eng.upload(file, TOTAL_NODES);
         const std::string& fileId = up.first;
-        std::printf("[%d] FileId = %s\n", u, fileId.c_str());
-        std::printf("[%d] Original name = %s\n", u, name.c_str());
+        out.printf("[%d] FileId = %s\n", u, fileId.c_str());
+        out.printf("[%d] Original name = %s\n", u, name.c_str());
         const int u0 = u - 1, my1 = u0, my2 = (u0 + 1) % TOTAL_NODES;
         for (const auto& f : up.second) {
-            std::printf("[%d] Fragment %d: %zu bytes, hash=%s\n", u, f.index, f.data.size(), f.hash.c_str());
+            out.printf("[%d] Fragment %d: %zu bytes, hash=%s\n", u, f.index, f.data.size(), f.hash.c_str());
             if (f.index == my1 || f.index == my2) {
                 node(u).saveFragment(fileId, f.index, f.data);  // SN:165-166
-                std::printf("[%d] Saved fragment %d locally\n", u, f.index);
+                out.printf("[%d] Saved fragment %d locally\n", u, f.index);
             }
         }
         // sendFragmentsToPeers (SN:195-224); every peer's body built on the device
@@ -178,7 +216,7 @@ struct Cluster {
             const int f1 = k, f2 = (k + 1) % TOTAL_NODES;
             bool ok = false;
             for (int attempt = 1; attempt <= 3 && !ok; ++attempt) {
-                std::printf("[%d] Sending fragments %d and %d to node %d (attempt %d)\n", u, f1, f2, k + 1, attempt);
+                out.printf("[%d] Sending fragments %d and %d to node %d (attempt %d)\n", u, f1, f2, k + 1, attempt);
                 try {
                     const std::string& body = bodies[j];
                     if (body != dfs::buildFragmentsJson(fileId, {&up.second[f1], &up.second[f2]}))
@@ -187,7 +225,7 @@ struct Cluster {
                     ok = true;
                     for (int fi : {f1, f2}) {  // SN:250-257
                         if (remote[fi] != up.second[fi].hash) {
-                            std::printf("[%d] Hash mismatch on fragment %d (local=%s, remote=%s)\n", u, fi,
+                            out.printf("[%d] Hash mismatch on fragment %d (local=%s, remote=%s)\n", u, fi,
                                         up.second[fi].hash.c_str(), remote[fi].c_str());
                             ok = false;
                         }
@@ -196,14 +234,17 @@ struct Cluster {
                 }
             }
             if (!ok) {
-                std::printf("[%d] FAILED sending to node %d\n", u, k + 1);
+                out.printf("[%d] FAILED sending to node %d\n", u, k + 1);
                 return "";  // 500 "Replication failed", SN:174-177
             }
             ++j;
         }
         const std::string manifest = dfs::buildManifestJson(fileId, name, TOTAL_NODES);
-        for (auto& n : nodes) n.manifests[fileId] = manifest;  // save + announce (SN:180-186)
-        std::printf("[%d] Uploaded %s\n", u, name.c_str());
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (auto& n : nodes) n.manifests[fileId] = manifest;  // save + announce (SN:180-186)
+        }
+        out.printf("[%d] Uploaded %s\n", u, name.c_str());
         return fileId;
     }
 
@@ -231,15 +272,22 @@ struct Cluster {
             }
             plan += (i ? "," : "") + src;
         }
-        return eng.reassembleAndVerify(fileId, frags);  // SN:448-458
+        return batcher ? dfs::FragmentEngine::reassembleAndVerify(batcher, fileId, frags)
+                       : eng.reassembleAndVerify(fileId, frags);  // SN:448-458
     }
 };
 
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc < 2) {
-        std::fprintf(stderr, "usage: %s <file>...\n", argv[0]);
+    bool threaded = true;
+    std::vector<std::string> paths;
+    for (int a = 1; a < argc; ++a) {
+        if (std::string(argv[a]) == "--serial") threaded = false;
+        else paths.push_back(argv[a]);
+    }
+    if (paths.empty()) {
+        std::fprintf(stderr, "usage: %s [--serial] <file>...\n", argv[0]);
         return 2;
     }
     std::string data;
@@ -264,47 +312,80 @@ int main(int argc, char** argv) {
         }
     } cleanup{data, keep};
     try {
-        Cluster c(data);
+        Cluster c(data, threaded);
         std::vector<std::pair<std::string, dfs::Bytes>> files;
-        std::vector<std::string> ids;
-        for (int a = 1; a < argc; ++a) {
-            std::ifstream in(argv[a], std::ios::binary);
-            if (!in) throw std::runtime_error(std::string("cannot read ") + argv[a]);
+        for (const std::string& p : paths) {
+            std::ifstream in(p, std::ios::binary);
+            if (!in) throw std::runtime_error("cannot read " + p);
             dfs::Bytes b((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-            files.emplace_back(basename_of(argv[a]), b);
-            const std::string id = c.upload(1, files.back().first, b);
-            if (id.empty()) return 1;
-            ids.push_back(id);
+            files.emplace_back(basename_of(p), b);
         }
+        const size_t nf = files.size();
+        // Run fn(k, log) for every file k: one handler thread per request
+        // (SN:30) or, with --serial, one after the other; then print the logs
+        // in request order.  An exception that escapes a handler is rethrown.
+        auto handlers = [&](auto fn) {
+            std::vector<Log> logs(nf);
+            std::vector<std::string> errs(nf);
+            auto run = [&](size_t k) {
+                try {
+                    fn(k, logs[k]);
+                } catch (const std::exception& e) {
+                    errs[k] = e.what();
+                }
+            };
+            if (threaded) {
+                std::vector<std::thread> th;
+                for (size_t k = 0; k < nf; ++k) th.emplace_back(run, k);
+                for (auto& t : th) t.join();
+            } else {
+                for (size_t k = 0; k < nf; ++k) run(k);
+            }
+            for (size_t k = 0; k < nf; ++k) std::fputs(logs[k].text.c_str(), stdout);
+            for (size_t k = 0; k < nf; ++k)
+                if (!errs[k].empty()) throw std::runtime_error(errs[k]);
+        };
+        std::vector<std::string> ids(nf);
+        handlers([&](size_t k, Log& log) { ids[k] = c.upload(1, files[k].first, files[k].second, log); });
+        for (const std::string& id : ids)
+            if (id.empty()) return 1;
         c.node(3).up = false;  // config 1: node 3 down after the uploads
         std::printf("[sim] node 3 is down\n");
-        int bad = 0;
+        std::vector<int> bad(nf, 0);
         for (int r : {1, 2, 4, 5}) {
-            for (size_t k = 0; k < files.size(); ++k) {
+            handlers([&](size_t k, Log& log) {
                 std::string plan;
                 try {
                     dfs::Bytes got = c.download(r, ids[k], plan);
                     const bool same = got == files[k].second;
-                    std::printf("[%d] Download %s fileId=%s plan=%s -> %zu bytes %s\n", r, files[k].first.c_str(),
-                                ids[k].c_str(), plan.c_str(), got.size(), same ? "OK" : "MISMATCH");
-                    bad += !same;
+                    log.printf("[%d] Download %s fileId=%s plan=%s -> %zu bytes %s\n", r, files[k].first.c_str(),
+                               ids[k].c_str(), plan.c_str(), got.size(), same ? "OK" : "MISMATCH");
+                    bad[k] += !same;
                 } catch (const dfs::DownloadError& e) {
-                    std::printf("[%d] Download %s -> 500 %s\n", r, files[k].first.c_str(), e.what());
-                    ++bad;
+                    log.printf("[%d] Download %s -> 500 %s\n", r, files[k].first.c_str(), e.what());
+                    ++bad[k];
                 }
-            }
+            });
         }
+        int nbad = 0;
+        for (int b : bad) nbad += b;
         // both holders of fragment 2 (nodes 3 and 2) down -> SN:443-446
         c.node(2).up = false;
         std::string plan;
         try {
             c.download(1, ids[0], plan);
             std::printf("[1] Download with nodes 2,3 down -> unexpectedly OK\n");
-            ++bad;
+            ++nbad;
         } catch (const dfs::DownloadError& e) {
             std::printf("[1] Download with nodes 2,3 down -> 500 %s\n", e.what());
         }
-        return bad ? 1 : 0;
+        if (c.batcher) {
+            dfs_batcher_stats_t st{};
+            dfs_batcher_stats(c.batcher, &st);
+            std::printf("[sim] batcher: %llu requests in %llu batches (largest %llu)\n",
+                        (unsigned long long)st.requests, (unsigned long long)st.batches, (unsigned long long)st.max_batch);
+        }
+        return nbad ? 1 : 0;
     } catch (const std::exception& e) {
         std::fprintf(stderr, "storage_node_sim: %s\n", e.what());
         return 3;

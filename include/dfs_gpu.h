@@ -435,6 +435,18 @@ int dfs_submit_upload(dfs_batcher* batcher, const uint8_t* file, uint64_t len, u
 int dfs_submit_download(dfs_batcher* batcher, const char* b64, const dfs_span* frags, uint64_t file_len,
                         const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest, uint8_t* out);
 
+/* One download as the reference has it (handleDownload, SN:419-458): the
+ * fragments arrive as RAW bytes (tryLoadFragmentLocal SN:463-469 or a peer's
+ * getFragment reply, SN:513-514), frags[i] / frag_len[i] in index order
+ * (nfrag of them).  They are appended in order into `out` (SN:448) and the
+ * rebuilt file is SHA-256ed (SN:454): file_digest_out (may be NULL) gets the
+ * digest.  Returns 0, DFS_E_MISSING (a NULL fragment of non-zero length:
+ * "Could not retrieve fragment i", SN:443-446, nothing is hashed) or
+ * DFS_E_CORRUPT (digest != expected_file_digest, SN:455-458; `out` is left
+ * untouched).  expected_file_digest may be NULL (not checked). */
+int dfs_submit_reassemble(dfs_batcher* batcher, const uint8_t* const* frags, const uint64_t* frag_len,
+                          const uint8_t* expected_file_digest, uint8_t* out, uint8_t* file_digest_out);
+
 /* ---- multi-GPU placement over RCCL / xGMI (SN:143-145, 195-259, 422-446) -- */
 /* One rank per GPU; node k (0-based) is hosted by rank k mod W (W = ranks).
  * Node k stores fragments {k, (k+1) mod N} (SN:143-145), so fragment f lives

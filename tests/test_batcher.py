@@ -166,3 +166,40 @@ def test_host_alloc_registry():
     assert L.lib().dfs_host_free(ctypes.c_void_p(p.value + 8)) == dfs_amd.DFS_E_ARG  # not an allocation start
     assert L.lib().dfs_host_free(p) == 0
     assert L.lib().dfs_host_free(p) == dfs_amd.DFS_E_ARG  # already freed
+
+
+def test_concurrent_raw_fragment_downloads_vs_oracle():
+    """dfs_submit_reassemble: handleDownload as the reference has it (SN:419-458,
+    raw fragments) from 48 handler threads at once, mixed with uploads in the
+    same batcher: the rebuilt bytes and digest against hashlib, a corrupted
+    fragment ("File corrupted", SN:455-458: the caller's buffer untouched), a
+    missing one ("Could not retrieve fragment", SN:443-446), empty files."""
+    import hashlib
+    nfrag = 5
+    with Batcher(0, nfrag, max_wait_us=2000) as b:
+        def work(t):
+            for k in range(3):
+                i = t * 3 + k
+                data = _file(i)
+                frags = [data[o:o + n] for o, n in O.c_split(len(data), nfrag)]
+                want = hashlib.sha256(data).digest()
+                st, back, dig = b.reassemble(frags, want)
+                assert st == 0 and back == data and dig == want, (i, st)
+                if t % 3 == 0:  # uploads interleave with the downloads in the queue
+                    fd, _, _ = b.upload(data)
+                    assert fd == want
+                if len(data) >= nfrag:
+                    bad = list(frags)
+                    bad[2] = bytes([bad[2][0] ^ 0x40]) + bad[2][1:]
+                    st, back, dig = b.reassemble(bad, want)
+                    assert st == dfs_amd.DFS_E_CORRUPT and back is None
+                    assert dig == hashlib.sha256(b"".join(bad)).digest()
+                    gone = list(frags)
+                    gone[4] = None
+                    st, back, dig = b.reassemble(gone, want)
+                    assert st == dfs_amd.DFS_E_MISSING and back is None
+                st, back, dig = b.reassemble(frags, None)  # nothing to compare with
+                assert st == 0 and back == data and dig == want
+        _run_threads(48, work)
+        s = b.stats()
+        assert s["requests"] >= 48 * 3 * 2 and s["max_batch"] > 1
