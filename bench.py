@@ -88,9 +88,11 @@ def parse(argv=None):
     ap.add_argument("--files", type=int, default=0, help="files per GPU (0 = the config's)")
     ap.add_argument("--file-size", type=int, default=0)
     ap.add_argument("--nfrag", type=int, default=0)
-    ap.add_argument("--mode", choices=("fused", "kernels", "serial"), default="kernels",
+    ap.add_argument("--mode", choices=("fused", "kernels", "serial", "hybrid"), default="kernels",
                     help="kernels: SHA and Base64 kernels on two streams (default); fused: Base64 "
-                         "written by the SHA fragment lanes; serial: the two kernels on one stream")
+                         "written by the SHA fragment lanes; hybrid: the fragment lanes write their own Base64, the "
+                         "encode kernel only that of the fragments hashed as twins inside their fileId lane; serial: "
+                         "the two kernels on one stream")
     ap.add_argument("--serial", action="store_true", help="alias of --mode serial")
     ap.add_argument("--align128", action=argparse.BooleanOptionalAction, default=True,
                     help="DFS_LAYOUT_ALIGN128: every fragment's Base64 starts on a 128-byte boundary")
@@ -207,6 +209,18 @@ def host_cpu_info():
     except (OSError, subprocess.SubprocessError):
         pass
     info["model"] = model
+    # physical cores lscpu reports (sockets x cores per socket): the box may
+    # show only its share of the machine
+    try:
+        sockets = cores_per = None
+        for line in out.splitlines():
+            if line.startswith("Socket(s)"):
+                sockets = int(line.split(":", 1)[1])
+            elif line.startswith("Core(s) per socket"):
+                cores_per = int(line.split(":", 1)[1])
+        info["physical_cores"] = sockets * cores_per if sockets and cores_per else None
+    except (NameError, ValueError):
+        info["physical_cores"] = None
     usable = aff if quota is None else max(1, min(aff, int(quota)))
     return info, usable
 
@@ -602,6 +616,27 @@ def batcher_leg(args, log):
 
     def cross(key, cpu_key):
         return next((r["clients"] for r in rows if r[cpu_key] and r[key]["gbps"] > r[cpu_key]), None)
+    # What the CPU path would reach on a whole host, as a projection: the
+    # measured single-thread rate x physical cores, linear scaling assumed
+    # (an upper bound: memory bandwidth and turbo are ignored).
+    info, _ = host_cpu_info()
+    one_up = next((r["cpu_upload_gbps"] for r in rows if r["cpu_threads"] == 1 and r["cpu_upload_gbps"]), None)
+    one_dn = next((r["cpu_download_gbps"] for r in rows if r["cpu_threads"] == 1 and r["cpu_download_gbps"]), None)
+    best_up = max((r["upload_pinned"]["gbps"] for r in rows), default=None)
+    best_dn = max((max(r["download_pinned"]["gbps"], r["download"]["gbps"]) for r in rows), default=None)
+    proj = None
+    if one_up and one_dn:
+        proj = {"single_thread_upload_gbps": one_up, "single_thread_download_gbps": one_dn, "hosts": []}
+        for label, ncores in (("this box as lscpu shows it", info.get("physical_cores")),
+                              ("a 2 x 64-core host (e.g. EPYC 9575F x2)", 128)):
+            if ncores:
+                proj["hosts"].append({"host": label, "cores": ncores, "upload_gbps": round(one_up * ncores, 1),
+                                      "download_gbps": round(one_dn * ncores, 1)})
+        proj["gpu_serving_best_gbps"] = {"upload": best_up, "download": best_dn}
+        proj["note"] = ("PROJECTION, not a measurement: single-thread CPU-proxy rate x cores.  The serving path moves "
+                        "every request over PCIe (1 MiB in + 1.33 MiB of Base64 out per upload: at most ~42 GB/s of "
+                        "file bytes on a 56 GB/s link), so a host with all its cores free would outrun it; the GPU wins "
+                        "where data is already in HBM (the headline step) or the host's cores are needed elsewhere")
     if not ok:
         raise LegError("batcher leg: a client result is wrong")
     return {"file_bytes": S, "nfrag": N, "rows": rows,
@@ -609,7 +644,7 @@ def batcher_leg(args, log):
                                   "download": cross("download", "cpu_download_gbps"),
                                   "upload_pinned": cross("upload_pinned", "cpu_upload_gbps"),
                                   "download_pinned": cross("download_pinned", "cpu_download_gbps")},
-            "ok": ok, "cpu_cores": cores,
+            "ok": ok, "cpu_cores": cores, "full_host_cpu_projection": proj,
             "note": "native client threads (tools/batcher_load, 3 workers, 2 ms window), host buffers: each request "
                     "crosses PCIe in and out; staged = pageable handler buffers copied by the handler into / out of "
                     "pinned staging, pinned = dfs_host_alloc buffers moved by DMA directly (direct = such requests); "
@@ -866,6 +901,7 @@ def multi_gpu(args, world, rank, local, log):
         ch0["held"][pos] = ord("B") if int(ch0["held"][pos]) == ord("A") else ord("A")
         probe[0], probe[1] = k, int(fr[k]["rank"])
     dist.broadcast(probe, src=0)
+    probe = probe.cpu()  # the broadcast is complete before the library's own communicator is used again
     verify_only()
     torch.cuda.synchronize(dev)
     want_failed = torch.zeros(world, dtype=torch.int32, device=dev)
@@ -1091,7 +1127,7 @@ def main():
         return 0 if ok else 3
 
     # read by dfs_open: two-kernel mode vs the fused SHA+Base64 kernel
-    os.environ["DFS_UPLOAD_MODE"] = "kernels" if args.mode != "fused" else "fused"
+    os.environ["DFS_UPLOAD_MODE"] = args.mode if args.mode in ("fused", "hybrid") else "kernels"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -1274,12 +1310,13 @@ def main():
                    "files_per_gpu": F, "file_bytes": S, "nfrag": N,
                    "mode": {"fused": "Base64 fused into the SHA-256 fragment lanes (one kernel)",
                             "kernels": "SHA-256 || Base64 kernels on two streams",
+                            "hybrid": "fragment lanes write their own Base64; Base64 kernel only for the twin fragments",
                             "serial": "SHA-256 then Base64 kernel, one stream"}[args.mode],
                    "b64_layout": "128-byte aligned fragment starts" if args.align128 else "packed"},
         "roofline": {"bound": "valu", "achieved": round(achieved_tops, 3), "peak": round(VALU_PEAK_TOPS, 3),
                      "unit": "Tops/s (int32)", "frac": round(achieved_tops / VALU_PEAK_TOPS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "sha256_lanes" + (" (+ fused Base64)" if args.mode == "fused" else ""),
+                     "kernel": "sha256_lanes" + (" (+ fused Base64)" if args.mode in ("fused", "hybrid") else ""),
                      "ms": round(sha_avg * 1e3, 3), "blocks_per_launch": blocks, "ops_per_block": OPS_PER_BLOCK_CANON,
                      "valu_issue_frac": round(issued_tops / VALU_PEAK_TOPS, 4)},
         "roofline_b64": {"bound": "hbm", "achieved": round(b64_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

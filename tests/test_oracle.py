@@ -171,3 +171,23 @@ def test_cpu_download_baseline_verifies():
         for ossl in (False, True):
             secs = O.cpu_download_bench(3, n, 5, 2, ossl)
             assert secs >= 0 or (ossl and secs == -1.0), (n, ossl, secs)
+
+
+def test_synth_digests_checker_matches_hashlib():
+    """oracle_synth_digests (the whole-batch checker of bench.py and the GPU
+    tests): fileId, fragment digests and the SHA-256 of each fragment's Base64
+    for synthetic files, libcrypto and scalar SHA-256 alike, against hashlib /
+    base64 on the same bytes — including files shorter than N (empty fragments)."""
+    import base64
+    import hashlib
+    for first, n, S, N in [(0, 5, 1000, 5), (77, 3, 3, 5), (9, 2, 0, 8), (1234, 4, 262144, 8), (5, 2, (1 << 20) + 1, 5)]:
+        for ossl in (True, False):
+            fd, frd, b64d = O.synth_digests(first, n, S, N, 3, use_openssl=ossl)
+            for f in range(n):
+                d = O.c_synth(first + f, 0, S)
+                assert fd[f].tobytes() == hashlib.sha256(d).digest()
+                for i, (o, ln) in enumerate(O.py_split(S, N)):
+                    assert frd[f, i].tobytes() == hashlib.sha256(d[o:o + ln]).digest()
+                    assert b64d[f, i].tobytes() == hashlib.sha256(base64.b64encode(d[o:o + ln])).digest()
+    fd, frd, none = O.synth_digests(0, 2, 100, 5, 1, with_b64=False)
+    assert none is None and fd.shape == (2, 32) and frd.shape == (2, 5, 32)

@@ -105,3 +105,72 @@ def test_twin_download(engine, mode, nfiles, size, nfrag, monkeypatch):
         assert st == want[f], f
         if want[f] == 0:
             assert body == files[f], f
+
+
+@pytest.fixture(scope="module")
+def hybrid_engine():
+    """DFS_UPLOAD_MODE=hybrid: the fragment lanes write their own Base64 in the
+    SHA pass and the encode kernel covers only the twins."""
+    import os
+    old = os.environ.get("DFS_UPLOAD_MODE")
+    os.environ["DFS_UPLOAD_MODE"] = "hybrid"
+    try:
+        eng = dfs_amd.FragmentEngine(0)
+    finally:
+        if old is None:
+            del os.environ["DFS_UPLOAD_MODE"]
+        else:
+            os.environ["DFS_UPLOAD_MODE"] = old
+    yield eng
+    eng.close()
+
+
+@pytest.mark.parametrize("nfiles,size,nfrag", SHAPES + [(33000, 4099, 5), (300, 70001, 3)])
+def test_hybrid_upload_uniform(hybrid_engine, nfiles, size, nfrag):
+    """Digests and Base64 of the hybrid upload against the oracle: launches with
+    twins (fragment 0, or every fragment) beside encoding fragment lanes, and
+    a small launch without twins (every fragment encoded by its own lane)."""
+    _check_upload(hybrid_engine, _files([size] * nfiles, nfiles + size + 1), nfrag)
+
+
+def test_hybrid_upload_ragged(hybrid_engine):
+    rng = np.random.default_rng(15)
+    n = 36000
+    sizes = rng.integers(0, 6000, n)
+    sizes[0::5] = 256 * rng.integers(1, 24, len(sizes[0::5]))
+    sizes[1::5] = 256 * rng.integers(1, 24, len(sizes[1::5])) + rng.integers(1, 4, len(sizes[1::5]))
+    sizes[2::97] = rng.integers(0, 256, len(sizes[2::97]))
+    sizes[3::1001] = 0
+    _check_upload(hybrid_engine, _files(sizes, 16), 4)
+
+
+@pytest.mark.parametrize("align128,frag_major", [(True, False), (False, True), (True, True)])
+def test_hybrid_upload_plan_device(hybrid_engine, align128, frag_major):
+    """The prepared plan on device buffers (the bench's path) in hybrid mode,
+    1 MiB-like geometry scaled down (fragments 1.. off the block grid): every
+    fileId, fragment digest and fragment Base64 (through its SHA-256) against
+    the oracle's C path over the same synthetic files; also without fileIds
+    (every fragment lane encodes, no encode kernel)."""
+    import torch
+    from dfs_amd.engine import sha256_device
+    nfiles, S, nfrag = 70000, 5 * 211 + 1, 5
+    spans = np.array([(f * S, S) for f in range(nfiles)], dtype=np.uint64)
+    files = torch.empty(nfiles * S + 64, dtype=torch.uint8, device="cuda")
+    dfs_amd.synth_fill(hybrid_engine, files.data_ptr(), spans, 31000, O.SYNTH_SEED)
+    plan = dfs_amd.UploadPlan(hybrid_engine, spans, nfrag, frag_major=frag_major, align128=align128)
+    efd, efrd, eb64 = O.synth_digests(31000, nfiles, S, nfrag, 8)
+    try:
+        for flags in (0, dfs_amd.DFS_NO_FILEID):
+            fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
+            frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
+            b64 = torch.zeros(plan.b64_total + 64, dtype=torch.uint8, device="cuda")
+            plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), flags)
+            torch.cuda.synchronize()
+            if not flags:
+                assert (fd.view(nfiles, 32).cpu().numpy() == efd).all()
+            assert (frd.view(nfiles, nfrag, 32).cpu().numpy() == efrd).all()
+            got = sha256_device(hybrid_engine, b64.data_ptr(), plan.b64_spans([S] * nfiles)).reshape(nfiles, nfrag, 32)
+            bad = np.argwhere((got != eb64).any(axis=2))
+            assert bad.size == 0, (flags, bad[:5].tolist())
+    finally:
+        plan.close()
