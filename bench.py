@@ -120,6 +120,9 @@ def parse(argv=None):
     ap.add_argument("--store-files", type=int, default=2048, help="files in the on-disk fragment store leg")
     ap.add_argument("--no-store", action="store_true", help="skip the on-disk fragment store leg")
     ap.add_argument("--no-batcher", action="store_true", help="skip the concurrent-clients (batcher) leg")
+    ap.add_argument("--no-scaling-ref", action="store_true",
+                    help="N=1: skip the leg that runs the N>1 step (upload + placement + holders' verify on BASELINE "
+                         "configs[2]'s shard) on this one GPU, the equal-workload reference for the N>1 lines")
     ap.add_argument("--clients", default="1,512,2048,4096", help="batcher leg: concurrent handler threads")
     ap.add_argument("--client-seconds", type=float, default=2.0, help="batcher leg: seconds per concurrency")
     ap.add_argument("--long-files", type=int, default=1024)
@@ -1364,6 +1367,42 @@ def main():
             traceback.print_exc()
             result["batcher"] = {"error": repr(e)[:600]}
             failures.append("batcher")
+    # The N > 1 lines measure another workload than this one (BASELINE
+    # configs[2]'s shard with placement and the holders' verify, not
+    # configs[1]): the same step on this one GPU (one-rank communicator, no
+    # bytes cross xGMI) is the equal-workload reference for them.  A child
+    # process, after this one has handed its buffers back.
+    if not args.no_scaling_ref and not args.placement_step and args.config == 2:
+        try:
+            if args.no_batcher:
+                plan.close()
+                del files, b64, fd, frd, legs
+                torch.cuda.synchronize(dev)
+                torch.cuda.empty_cache()
+            cmd = [sys.executable, os.path.abspath(__file__), "--placement-step", "--steps", "5", "--warmup", "2",
+                   "--placement", args.placement]
+            p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+            if p.returncode != 0 or not line:
+                raise LegError(f"placement-step child rc {p.returncode}: {p.stderr[-300:]}")
+            r = json.loads(line[-1])
+            pl = r["placement"]
+            result["n_gt_1_step_on_one_gpu"] = {
+                "value": r["value"], "unit": "GB/s", "ms_per_step": r["ms_per_step"], "workload": r["config"]["workload"],
+                "compute_only_ms": pl["compute_only_ms"], "receive_verify_ms": pl["receive_verify_ms"],
+                "step_without_verify_ms": pl["step_without_verify_ms"], "verified": r["verified"],
+                "note": "bench.py --placement-step: the step the N>1 lines time, on a one-rank communicator (placement "
+                        "= local copies).  Weak-scaling efficiency on equal workloads = value(N) / (N x this value); "
+                        "the headline `value` above is BASELINE configs[1], which has no placement step"}
+            log(f"N>1 step on one GPU: {r['value']} GB/s, {r['ms_per_step']} ms per step")
+            if not r["verified"]:
+                failures.append("n_gt_1_step_on_one_gpu")
+        except Exception as e:
+            import traceback
+            traceback.print_exc()
+            result["n_gt_1_step_on_one_gpu"] = {"error": repr(e)[:300]}
+            failures.append("n_gt_1_step_on_one_gpu")
+        args.no_batcher = False  # the upload plan is closed
     if failures:
         result["failed_legs"] = failures
     emit(result)
