@@ -738,6 +738,7 @@ class Shard:
         bounds = [F * c // C for c in range(C + 1)]
         self.chunks = []
         raw_max = 0
+        self.replica_plan_ms = 0.0
         for c in range(C):
             a, b = bounds[c], bounds[c + 1]
             spans = np.stack([np.arange(a, b, dtype=np.uint64) * np.uint64(S),
@@ -747,7 +748,9 @@ class Shard:
             grp = [int(offs[f]) for f in range(N)] + [int(offs[-1])]
             # replica receiver's plan of this chunk (a collective: every rank's
             # file lengths are gathered); its table is what dfs_place_sizes gathers
+            t0 = time.perf_counter()
             rp = P.ReplicaPlan(comm, N, [S] * (b - a), align128=args.align128)
+            self.replica_plan_ms += (time.perf_counter() - t0) * 1e3
             table = rp.table
             if table[comm.rank].tolist() != [grp[f + 1] - grp[f] for f in range(N)]:
                 raise LegError("replica plan: group sizes differ from the upload plan's")
@@ -1002,6 +1005,7 @@ def multi_gpu(args, world, rank, local, log):
             "receive_verify_ms": round(t_verify * 1e3, 3),
             "step_without_verify_ms": round(t_noverify * 1e3, 3),
             "receive_verify": {"held_fragments_per_gpu": held_frags, "decoded_bytes_per_gpu": raw_bytes,
+                               "plan_ms": round(sh.replica_plan_ms, 2),
                                "all_replicas_good": verify_ok, "corrupt_probe_caught": probe_ok,
                                "note": "inside the timed step: every rank's fragment digests to the holders "
                                        "(dfs_replica_exchange, RCCL), each holder Base64-decodes and SHA-256s every "
