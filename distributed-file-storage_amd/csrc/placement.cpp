@@ -492,7 +492,7 @@ int dfs_place_plan(uint32_t nranks, uint32_t rank, uint32_t nfrag, const uint64_
     if (frag_status) std::memcpy(frag_status, p.status.data(), 4ull * nfrag);
     if (ops) {
         if (cap < p.ops.size()) return DFS_E_ARG;
-        std::memcpy(ops, p.ops.data(), sizeof(dfs_xfer) * p.ops.size());
+        if (!p.ops.empty()) std::memcpy(ops, p.ops.data(), sizeof(dfs_xfer) * p.ops.size());
     }
     return DFS_OK;
 }

@@ -177,7 +177,7 @@ int dfs_replica_layout(uint32_t nranks, uint32_t rank, uint32_t nfrag, const uin
     if (raw_bytes) *raw_bytes = L.raw_bytes;
     if (frags) {
         if (cap < L.frags.size()) return DFS_E_ARG;
-        std::memcpy(frags, L.frags.data(), sizeof(dfs_held_frag) * L.frags.size());
+        if (!L.frags.empty()) std::memcpy(frags, L.frags.data(), sizeof(dfs_held_frag) * L.frags.size());
     }
     return DFS_OK;
 }
