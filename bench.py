@@ -51,7 +51,7 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-file-storage_amd"))
 
 METRIC = "SHA-256+Base64 fragment GB/s per node at 1/8 GPUs; % of int-VALU peak"
 SEED = 0x5EED5EED
-# canonical int32 VALU ops per 64-byte SHA-256 block (gfx950
+# Canonical int32 VALU ops per 64-byte SHA-256 block, the count the roofline is priced with (gfx950
 # ISA without v_xor3).  The shipped kernel issues 1,405 (v_bitop3 folds the
 # three-input XORs), so `frac` below is algorithmic, not issue utilisation;
 # `valu_issue_frac` gives the executed-instruction view.
@@ -888,7 +888,7 @@ def multi_gpu(args, world, rank, local, log):
     torch.cuda.synchronize(dev)
     verify_ok = verify_clean()  # every replica of every step's last run checked good on its holder
     side = max(1, min(args.steps, 3))
-    # the same step without the holders' verify (round 2's step), without any
+    # the same step without the holders' verify, without any
     # exchange, the verify alone, and each placement alone
     t_noverify = timed(lambda: step(args.placement, verify=False), side)
     t_comp = timed(lambda: step(args.placement, place=False), side)
@@ -1215,7 +1215,7 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
 
-    # ---- fragment-only variant (SURVEY §8d): no fileId SHA-256 (SN:127)
+    # ---- fragment-only variant: no fileId SHA-256 (SN:127)
     frag_only = None
     if args.frag_only_steps:
         eng.set_profiling(True)

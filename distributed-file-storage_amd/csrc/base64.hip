@@ -6,7 +6,7 @@
 // handleInternalStoreFragments (StorageNode.java:281), including the JDK
 // basic decoder's IllegalArgumentException cases.
 //
-// Both kernels are HBM-bound byte streams (DESIGN.md §3.2): 12 input bytes
+// Both kernels are HBM-bound byte streams: 12 input bytes
 // -> 16 chars per lane-step, 64 lanes of a wave touch 768 contiguous input
 // bytes and 1 KiB of contiguous output, the 6-bit -> ASCII map (and its
 // inverse) is a table in LDS, and misaligned starts are fixed in registers
@@ -208,8 +208,8 @@ __device__ __forceinline__ uint32_t dec_unit_bytes(const uint8_t* __restrict__ l
 // group), decodes the final unit (every lane, same address: a broadcast
 // load), writes the head bytes [0, h) and tail bytes [h + 16 nchunks, total)
 // — at most 15 + 28, one byte per lane, all loads in flight at once — and
-// sets status / out_len (SN:281's IllegalArgumentException cases, DESIGN.md
-// §3.2).
+// sets status / out_len (SN:281's IllegalArgumentException cases: a char
+// outside the alphabet, a 1-char final unit, wrong padding).
 __device__ __forceinline__ void dec_tail(const uint8_t* __restrict__ lut, const StreamJob& job, const DecGeom& G,
                                       const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                       int32_t* __restrict__ status, uint64_t* __restrict__ out_len) {

@@ -15,7 +15,8 @@
 // and out of the pinned staging, so those copies run in parallel instead of
 // on the worker.  Host-resident data crosses PCIe twice (file in, Base64
 // out for uploads; Base64 in, file out for downloads): that, not the
-// kernels, bounds a host-buffer caller at high concurrency.
+// kernels, bounds a host-buffer caller at high concurrency (an upload is
+// capped near 42 GB/s of file bytes on a 56 GB/s link).
 //
 // Hand-off per request:
 //   0 queued -> 1 worker assigned its staging slot (in_dst) -> 2 handler

@@ -7,7 +7,7 @@
 // a download takes fragment i locally, else from node i, else from node i-1
 // (:422-440), and fails with "Could not retrieve fragment i" (:443-446).
 //
-// MI355X mapping (DESIGN.md §5): one rank per GPU, node k hosted by rank
+// MI355X mapping: one rank per GPU, node k hosted by rank
 // k mod W.  A rank's Base64 is fragment-major: group f = the Base64 of
 // fragment f of every file the rank uploaded, groups back to back.  After a
 // placement every rank holds, for each fragment f it hosts, "held group f" =

@@ -4,7 +4,7 @@
 // sha256Hex call site of StorageNode.java (SN:127 fileId, SN:159 fragment,
 // SN:282 received fragment, SN:454 download verify).  FIPS 180-4.
 //
-// Design (DESIGN.md §3.1):
+// Design:
 //  * One message per lane.  SHA-256 is a strict chain within a message, so
 //    the parallelism is across messages (files' fragments and fileIds).
 //  * Lanes are pre-sorted by length (longest first) on the host so waves are
@@ -198,7 +198,7 @@ __device__ __forceinline__ void init_state(uint32_t (&st)[8]) {
 // and the next pair is in flight while the current pair is compressed (two
 // pairs of register buffers, loop unrolled x4).  Beside the Base64 stream
 // this cut the SHA kernel's re-reads and its stalls on loaded HBM
-// (DESIGN.md §3.1).
+// (154 GB read per config-2 launch against 198 GB with one-block-ahead fetch).
 __device__ __forceinline__ void plain_range(uint32_t (&st)[8], const Msg& m, uint32_t kb, uint32_t ke) {
     uint32_t A[16], B[16], C[16], D[16], xa, xb, xc, xd;
     const uint32_t last = ke - 1u;
@@ -829,7 +829,7 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
         uint32_t *__restrict__ queue, uint32_t *__restrict__ state, char *__restrict__ b64, ShaWait wait
 // Plain (hash only).  The pair-fetch block loop measured 76.6 ms alone on
 // config 2 (78.8 ms with two register buffers, 79.4 ms with one compression
-// per iteration); beside Base64 91.3 / 93.1 / 93.9 ms (DESIGN.md §3.1).
+// per iteration); beside Base64 91.3 / 93.1 / 93.9 ms.
 __global__ __launch_bounds__(kShaBlock) void sha256_lanes(DFS_SHA_ARGS) {
     sha256_body<false, false>(base, descs, n, split, n_long, cap, out0, out1, queue, state, b64, wait);
 }

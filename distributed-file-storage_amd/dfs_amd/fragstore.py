@@ -28,7 +28,7 @@ def _ptr(a: np.ndarray) -> int:
 def _order_after_torch(engine) -> None:
     """Device-mode store calls copy on the engine's ctx stream, which nothing
     orders after torch's current stream: finish the producer (or consumer
-    fill) queued on torch's stream first (ADVICE r1).  A caller that set the
+    fill) queued on torch's stream first.  A caller that set the
     ctx stream to torch's own stream (engine.set_stream) is ordered already."""
     import torch
     if torch.cuda.is_available():

@@ -80,7 +80,7 @@ def download_sources(n: int, world: int, me: int, offline: Iterable[int] = ()) -
 
 
 def file_owner(file_digest, world: int):
-    """Lookup rank of files after the upload: files are
+    """Lookup rank of files after the upload (BASELINE configs[2], "sharded by fileId"): files are
     sharded by index for hashing, but a later GET /download?fileId=<hex>
     (SN:399-403) only knows the fileId, so the owner is the digest's first 8
     bytes (big-endian, the first 16 hex chars) mod world.  file_digest:

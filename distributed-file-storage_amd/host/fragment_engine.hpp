@@ -12,7 +12,7 @@
 //   parseResponseHashes check     SN:248-257   ("Hash mismatch on fragment")
 //   handleDownload gather+verify  SN:419-461   ("Could not retrieve fragment i",
 //                                               "File corrupted")
-// A Java build binds the same C ABI through FFM/JNI.
+// A Java build binds the same C ABI through FFM (java.lang.foreign) or JNI.
 #pragma once
 
 #include <cstdint>

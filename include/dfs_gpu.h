@@ -6,7 +6,7 @@
  * cited as SN:line).  The reference has no plugin/FFI API: its hot path is
  * private methods and JDK calls.  Each entry point below replaces the listed
  * reference sites; a Java host binds them through FFM (java.lang.foreign) or
- * JNI as shown in INTEGRATION.md.  HTTP routes, JSON bodies, manifest.json and
+ * JNI.  HTTP routes, JSON bodies, manifest.json and
  * the on-disk layout are unchanged.
  *
  * Conventions

@@ -276,7 +276,7 @@ int oracle_reassemble_verify(const uint8_t* const* src, const uint64_t* len, uin
 }
 
 /* ------------------------------------------------------------------ */
-/* Synthetic data: counter-based splitmix64.           */
+/* Synthetic data: counter-based splitmix64.                            */
 /* ------------------------------------------------------------------ */
 static uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9e3779b97f4a7c15ull;

@@ -11,8 +11,7 @@ tests/golden/examples/), FIPS 180-4 / RFC 4648 known answers, edge sizes and
 the synthetic generator.  There is no JDK in this image, so the reference
 itself could not be run: digests and Base64 are pinned by the standards the
 JDK classes implement; decoder error cases are restated JDK semantics
-(java.util.Base64.Decoder, basic) and are marked "parity unpinned" in
-DESIGN.md.
+(java.util.Base64.Decoder, basic) and are "parity unpinned": never run on a JDK.
 
 Run:  python oracle/gen_golden.py   (rewrites tests/golden/golden.json)
 """
@@ -104,7 +103,7 @@ def main():
         r = O.py_b64_decode_jdk(t)
         g["b64_decode_jdk"].append({"input_hex": t.hex(), "output_hex": None if r is None else r.hex()})
 
-    # The reference's examples/ files at N=5 (SURVEY Appendix A.1).
+    # The reference's examples/ files at N=5.
     g["examples"] = []
     for name in ["teste.txt", "id.jpg", "pl.png", "pag1.html"]:
         data = open(os.path.join(EX_DIR, name), "rb").read()

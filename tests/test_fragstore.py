@@ -128,7 +128,7 @@ def test_bad_arguments(tmp_path):
                                          0) == L.DFS_E_ARG
     assert lib.dfs_store_read_fragments(None, str(tmp_path).encode(), dig.ctypes.data, 1, None, refs.ctypes.data, 1,
                                         None, st.ctypes.data, 0) == L.DFS_E_ARG
-    # a ref naming a file past the digest table (ADVICE r1): rejected before any I/O
+    # a ref naming a file past the digest table: rejected before any I/O
     data4 = np.zeros(4, dtype=np.uint8)
     bad = make_refs([0], [4], [1], [0])
     assert lib.dfs_store_write_fragments(None, str(tmp_path).encode(), dig.ctypes.data, 1, data4.ctypes.data,

@@ -537,8 +537,8 @@ def test_profiling_timings(engine):
 def test_storage_node_sim_config1(golden, tmp_path, handlers):
     """BASELINE config 1 replayed through the C++ host mirror: 5 nodes, upload
     examples/* at node 1, node 3 down, download at nodes 1, 2, 4, 5.  The
-    fragment log lines must equal the golden ones and the
-    fetch plans the reference's; every node's data directory
+    fragment log lines must equal the golden ones and the fetch plans the
+    reference's (SN:422-440); every node's data directory
     holds exactly its pair as raw .frag files (SN:143-145, 163-166, 284-285).
     threads (the default): one handler thread per request as in the reference
     (SN:28-31), the four uploads at once and then each node's four downloads

@@ -1,8 +1,8 @@
 """The CPU oracle pinned against the golden vectors (no GPU).
 
 Golden vectors: FIPS 180-4 / RFC 4648 known answers, the reference's own
-examples/ files, edge sizes on synthetic data, the JDK
-decoder's accept/reject cases (restated semantics).
+examples/ files, edge sizes on synthetic data, the JDK decoder's accept/reject
+cases (restated semantics: parity unpinned, no JDK here to run them on).
 """
 import base64
 import hashlib
@@ -41,8 +41,8 @@ def test_b64_decode_jdk_cases(golden):
 
 
 def test_survey_appendix_a_values(golden):
-    # A few values transcribed from SURVEY.md Appendix A.1 (computed there
-    # with hashlib and cross-checked with sha256sum / openssl dgst).
+    # A few values of the reference's example files, computed independently
+    # with hashlib and cross-checked with sha256sum / openssl dgst.
     ex = {e["name"]: e for e in golden["examples"]}
     assert ex["teste.txt"]["fileId"] == "3915569114252388ab0ede1637a7ca2c871d7785311389a22d10a13a71d662a3"
     assert ex["id.jpg"]["fileId"] == "020122de5ef7472f33fb6bc9c9b5fe49377f96f0cb37180a58a48b04b5bfdff2"

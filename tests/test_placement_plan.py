@@ -81,7 +81,7 @@ def test_degraded_fetch(world, nfrag):
 
 
 def test_node3_down_plan_matches_reference_table():
-    """5 nodes on 5 ranks, node 3 (rank 2) down."""
+    """The reference's fetch plan (SN:422-440) for 5 nodes on 5 ranks with node 3 (rank 2) down."""
     table = np.full((5, 5), 10, dtype=np.uint64)
     want = {0: [None, None, 1, 3, 4], 1: [0, None, None, 3, 4], 3: [0, 1, 1, None, None], 4: [None, 1, 1, 3, None]}
     for q, row in want.items():

@@ -1,6 +1,6 @@
 """storeFragments wire codec, sender side: dfs_store_bodies_build vs the
 oracle's buildFragmentsJson restatement (SN:629-642) and the golden bodies of
-the reference's examples (SURVEY Appendix A.1, uploaded at node 1).
+the reference's examples (uploaded at node 1).
 
 Bar: byte-identical request bodies.  The CPU test covers the length helper;
 the GPU tests build the bodies on the device through the C ABI."""

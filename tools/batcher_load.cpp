@@ -40,7 +40,7 @@ uint64_t splitmix64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-// The bench's synthetic file f (dfs_synth_fill's byte stream, BASELINE.md §3).
+// The bench's synthetic file f (dfs_synth_fill's byte stream).
 void synth(uint64_t f, uint64_t len, uint8_t* out) {
     for (uint64_t o = 0; o < len; o += 8) {
         const uint64_t v = splitmix64(kSeed ^ ((f << 40) | (o >> 3)));

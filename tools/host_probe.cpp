@@ -1,4 +1,4 @@
-// host_probe.cpp — host-side costs behind the request batcher (DESIGN.md §3.7):
+// host_probe.cpp — host-side costs behind the request batcher:
 //  1. memcpy rate between pageable and pinned (hipHostMalloc) memory, 1 and
 //     T threads (a handler's copy in / out of the staging);
 //  2. thread CPU time a caller spends per dfs_upload_batch of one 1 MiB file
