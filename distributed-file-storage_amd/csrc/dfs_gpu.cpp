@@ -76,7 +76,7 @@ struct dfs_ctx {
     uint32_t ovl_dec_wgs = 1;    // ... and decode workgroups per CU beside them (DFS_OVL_DEC_WGS); both
                                  // clamped at open so the two grids are resident together (ovl_fit)
     uint32_t ovl_gather_wgs = 2; // gather workgroups per CU beside them (reassembly overlap; fitted too)
-    int b64_wgs = 1;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
+    int b64_wgs = 2;             // encode workgroups per CU beside SHA (DFS_B64_WGS)
     uint32_t b64_prio = 1;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO; profiles/r02c_knobs)
     uint32_t dec_prio = 1;       // decode waves at s_setprio 3 beside SHA (DFS_DEC_PRIO=0: 0)
     uint32_t dec_wgs = 1;        // decode workgroups per CU beside SHA (DFS_DEC_WGS)
