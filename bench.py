@@ -561,10 +561,13 @@ def batcher_leg(args, log):
     """Thread-per-connection clients (SN:28-31), one 1 MiB file per request,
     through the library's batcher (dfs_submit_upload / dfs_submit_download,
     host buffers: PCIe in and out) at each concurrency in --clients, closed
-    loop for --client-seconds, in two buffer modes: "staged" (pageable
+    loop for --client-seconds, in three buffer modes: "staged" (pageable
     handler buffers: each handler copies its bytes into and out of the
-    worker's pinned staging) and "pinned" (handler buffers from
-    dfs_host_alloc: the worker's DMA reads / writes them, no host copies).
+    worker's pinned staging), "pinned" (handler buffers from
+    dfs_host_alloc: the worker's DMA reads / writes them, no host copies) and
+    "view" (pinned inputs; the answer stays in the batch's pinned result
+    buffer and the handler gets a pointer: dfs_submit_*_view, one DMA out per
+    batch instead of one per request).
     The clients are native threads (tools/batcher_load, a child process); the
     fileIds it reports are checked here.  Beside it the CPU proxy at the same
     concurrency (min(C, cores) threads, one file per thread), upload and
@@ -579,7 +582,7 @@ def batcher_leg(args, log):
     rows, ok, cpu_one = [], True, None
     for C in [int(x) for x in args.clients.split(",") if x]:
         row = {"clients": C}
-        for pinned in (0, 1):
+        for pinned in (0, 1, 2):
             for kind in ("upload", "download"):
                 p = subprocess.run([tool, str(C), str(args.client_seconds), kind, str(S), str(N), "2000", "3",
                                     str(pinned)], capture_output=True, text=True, timeout=300)
@@ -588,11 +591,13 @@ def batcher_leg(args, log):
                                    f"{p.stdout[-300:]}")
                 r = json.loads(p.stdout.strip().splitlines()[-1])
                 ok &= r["ok"] and [r["file0_id"], r["file1_id"]] == want
-                key = kind + ("_pinned" if pinned else "")
+                key = kind + ("", "_pinned", "_view")[pinned]
                 row[key] = {k: r[k] for k in ("requests", "gbps", "p50_ms", "p99_ms")}
                 st = r["stats"]
                 row[key]["batches"] = st["batches"]
                 row[key]["direct"] = st["direct"]
+                if pinned == 2:
+                    row[key]["views"] = st["views"]
                 row[key]["mean_batch"] = round(st["requests"] / max(st["batches"], 1), 1)
                 row[key]["device_ms_per_batch"] = round(st["device_s"] / max(st["batches"], 1) * 1e3, 2)
                 row[key]["client_cpu_us_per_req"] = round(r["client_cpu_us_per_req"]["in_submit"], 1)
@@ -612,10 +617,11 @@ def batcher_leg(args, log):
         if cpu_one:  # one handler's file, queued behind C / threads others
             row["cpu_latency_est_ms"] = round(cpu_one * 1e3 * ((C + th_cpu - 1) // th_cpu), 2)
         rows.append(row)
-        log(f"batcher: {C} clients: upload {row['upload']['gbps']} / pinned {row['upload_pinned']['gbps']} GB/s "
-            f"p50 {row['upload_pinned']['p50_ms']} ms (batch {row['upload_pinned']['mean_batch']}), download "
-            f"{row['download']['gbps']} / pinned {row['download_pinned']['gbps']} GB/s; cpu {row['cpu_upload_gbps']} / "
-            f"{row['cpu_download_gbps']}")
+        log(f"batcher: {C} clients: upload {row['upload']['gbps']} / pinned {row['upload_pinned']['gbps']} / view "
+            f"{row['upload_view']['gbps']} GB/s p50 {row['upload_view']['p50_ms']} ms (batch "
+            f"{row['upload_view']['mean_batch']}), download {row['download']['gbps']} / pinned "
+            f"{row['download_pinned']['gbps']} / view {row['download_view']['gbps']} GB/s; cpu "
+            f"{row['cpu_upload_gbps']} / {row['cpu_download_gbps']}")
 
     def cross(key, cpu_key):
         return next((r["clients"] for r in rows if r[cpu_key] and r[key]["gbps"] > r[cpu_key]), None)
@@ -625,8 +631,9 @@ def batcher_leg(args, log):
     info, _ = host_cpu_info()
     one_up = next((r["cpu_upload_gbps"] for r in rows if r["cpu_threads"] == 1 and r["cpu_upload_gbps"]), None)
     one_dn = next((r["cpu_download_gbps"] for r in rows if r["cpu_threads"] == 1 and r["cpu_download_gbps"]), None)
-    best_up = max((r["upload_pinned"]["gbps"] for r in rows), default=None)
-    best_dn = max((max(r["download_pinned"]["gbps"], r["download"]["gbps"]) for r in rows), default=None)
+    best_up = max((max(r[k]["gbps"] for k in ("upload", "upload_pinned", "upload_view")) for r in rows), default=None)
+    best_dn = max((max(r[k]["gbps"] for k in ("download", "download_pinned", "download_view")) for r in rows),
+                  default=None)
     proj = None
     if one_up and one_dn:
         proj = {"single_thread_upload_gbps": one_up, "single_thread_download_gbps": one_dn, "hosts": []}
@@ -646,11 +653,15 @@ def batcher_leg(args, log):
             "crossover_clients": {"upload": cross("upload", "cpu_upload_gbps"),
                                   "download": cross("download", "cpu_download_gbps"),
                                   "upload_pinned": cross("upload_pinned", "cpu_upload_gbps"),
-                                  "download_pinned": cross("download_pinned", "cpu_download_gbps")},
+                                  "download_pinned": cross("download_pinned", "cpu_download_gbps"),
+                                  "upload_view": cross("upload_view", "cpu_upload_gbps"),
+                                  "download_view": cross("download_view", "cpu_download_gbps")},
             "ok": ok, "cpu_cores": cores, "full_host_cpu_projection": proj,
             "note": "native client threads (tools/batcher_load, 3 workers, 2 ms window), host buffers: each request "
                     "crosses PCIe in and out; staged = pageable handler buffers copied by the handler into / out of "
-                    "pinned staging, pinned = dfs_host_alloc buffers moved by DMA directly (direct = such requests); "
+                    "pinned staging, pinned = dfs_host_alloc buffers moved by DMA directly (direct = such requests), view = pinned "
+                    "inputs, the answer left in the batch's pinned result buffer and handed out as a pointer "
+                    "(dfs_submit_*_view: one DMA out per batch); "
                     "latency = one handler's blocking call; cpu = the oracle's C proxy with min(C, cores) threads "
                     "(OpenSSL SHA-256 + scalar Base64, upload and download sequences); cpu_latency_est = one file's "
                     "single-thread time x ceil(C / threads); crossover = fewest clients where the GPU path beats the "

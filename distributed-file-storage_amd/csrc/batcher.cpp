@@ -18,6 +18,12 @@
 // kernels, bounds a host-buffer caller at high concurrency (an upload is
 // capped near 42 GB/s of file bytes on a 56 GB/s link).
 //
+// A request's output goes back one of three ways: copied by its handler out
+// of the batch's pinned result buffer (pageable callers), written by a DMA
+// of its own into its pinned buffer (direct), or left in the result buffer
+// and handed out as a pointer (dfs_submit_*_view: one DMA per batch, no host
+// copy; the buffer is reused only after every view of it was released).
+//
 // Hand-off per request:
 //   0 queued -> 1 worker assigned its staging slot (in_dst) -> 2 handler
 //   copied its input in (BatchSync::copied_in) -> 3 results ready (out_src,
@@ -125,7 +131,12 @@ struct Req {
     uint8_t* in_dst = nullptr;         // staging slot of the input
     const uint8_t* out_src = nullptr;  // staging of the output
     int status = DFS_OK;
-    bool direct = false;  // input and output in dfs_host_alloc buffers: DMA'd by the worker, no staging
+    bool direct = false;  // input (and, unless a view is asked for, output) in dfs_host_alloc buffers: DMA'd, no staging
+    // output as a view of the batch's result buffer (dfs_submit_*_view)
+    bool want_view = false;
+    const void** view_ptr = nullptr;
+    dfs_view** view_handle = nullptr;
+    dfs_view* view = nullptr;  // set by the worker when the batch succeeded (one reference is this request's)
     std::mutex mu;  // guards phase (and the fields the phase publishes)
     std::condition_variable cv;
 };
@@ -163,14 +174,35 @@ struct Buf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+}  // namespace
+
+// A batch's results in pinned memory.  `refs` counts the views handed out of
+// it; the worker that owns it takes it for a new batch only at zero.
+struct dfs_view {
+    std::mutex mu;
+    std::condition_variable cv;
+    int refs = 0;
+    Buf pin;
+    dfs_view() { pin.pinned = true; }
+};
+
+namespace {
+
 struct Worker {
     dfs_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // polled with sleeps (dfs::quiet_wait): the worker does not spin on the CPU share
-    Buf pin_in, pin_out, d_in, d_out, d_dig;
+    Buf pin_in, d_in, d_out, d_dig;
+    dfs_view outs[2];  // result buffers, alternating: batch k's views may outlive batch k + 1
+    int out_i = 0;
     std::thread th;
-    Worker() {
-        pin_in.pinned = pin_out.pinned = true;
+    Worker() { pin_in.pinned = true; }
+    // The result buffer of the next batch, once no view of it is left.
+    dfs_view* next_out() {
+        dfs_view* v = &outs[out_i ^= 1];
+        std::unique_lock<std::mutex> lk(v->mu);
+        v->cv.wait(lk, [&] { return v->refs == 0; });
+        return v;
     }
 };
 
@@ -239,16 +271,42 @@ void stage_in(dfs_batcher* B, std::vector<Req*>& batch, size_t staged, BatchSync
     tm.stage_in = since(t0);
 }
 
-// Staged requests first (their bytes form one contiguous prefix of the
-// staging and device buffers: one DMA each way), direct ones after.
-size_t order_batch(std::vector<Req*>& batch) {
-    auto mid = std::stable_partition(batch.begin(), batch.end(), [](const Req* r) { return !r->direct; });
-    return static_cast<size_t>(mid - batch.begin());
+// Order a batch so that the requests whose input is staged form a prefix
+// (one DMA in) and so do those whose output leaves through the result buffer
+// (staged or view: one DMA out): staged, staged + view, direct + view,
+// direct.  Returns the two prefix lengths.
+struct Prefix {
+    size_t in = 0, out = 0;
+};
+Prefix order_batch(std::vector<Req*>& batch) {
+    auto cls = [](const Req* r) { return r->direct ? (r->want_view ? 2 : 3) : (r->want_view ? 1 : 0); };
+    std::stable_sort(batch.begin(), batch.end(), [&](const Req* a, const Req* b) { return cls(a) < cls(b); });
+    Prefix p;
+    for (const Req* r : batch) {
+        p.in += !r->direct;
+        p.out += !r->direct || r->want_view;
+    }
+    return p;
+}
+
+// Hand the batch's views out (the batch succeeded): one reference each.
+void grant_views(std::vector<Req*>& batch, dfs_view* v) {
+    int n = 0;
+    for (Req* r : batch)
+        if (r->want_view) {
+            r->view = v;
+            ++n;
+        }
+    if (n) {
+        std::lock_guard<std::mutex> lk(v->mu);
+        v->refs += n;
+    }
 }
 
 int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs, Timing& tm) {
     const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
-    const size_t staged = order_batch(batch);
+    const Prefix pre = order_batch(batch);
+    const size_t staged = pre.in;
     std::vector<dfs_span> spans(n);
     std::vector<uint64_t> in_off(n);
     uint64_t total = 0, b64_total = 0, staged_in = 0, staged_b64 = 0;
@@ -257,11 +315,13 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
         spans[i] = dfs_span{total, batch[i]->len};
         total += (batch[i]->len + 15) & ~15ull;  // 16-byte aligned file starts
         b64_total += batch[i]->b64_off[N];       // filled at submit: the request's Base64 bytes
-        if (i + 1 == staged) staged_in = total, staged_b64 = b64_total;
+        if (i + 1 == pre.in) staged_in = total;
+        if (i + 1 == pre.out) staged_b64 = b64_total;
     }
     const uint64_t dig_bytes = 32ull * n * (N + 1);
+    dfs_view* res = w.next_out();
     int rc = w.pin_in.grow(staged_in + 16);
-    if (!rc) rc = w.pin_out.grow(dig_bytes + staged_b64 + 16);
+    if (!rc) rc = res->pin.grow(dig_bytes + staged_b64 + 16);
     if (!rc) rc = w.d_in.grow(total + 16);
     if (!rc) rc = w.d_out.grow(b64_total + 16);
     if (!rc) rc = w.d_dig.grow(dig_bytes);
@@ -285,12 +345,12 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
     rc = dfs_upload_batch(w.ctx, w.d_in.as<uint8_t>(), spans.data(), n, N, d_fd, d_frd, w.d_out.as<char>(),
                           b64_total, b64_off.data(), DFS_DEVICE_PTRS | DFS_SERIAL);
     if (rc) return rc;
-    uint8_t* h = w.pin_out.as<uint8_t>();
+    uint8_t* h = res->pin.as<uint8_t>();
     if (hipMemcpyAsync(h, d_fd, dig_bytes, hipMemcpyDeviceToHost, w.stream) != hipSuccess ||
         (staged_b64 && hipMemcpyAsync(h + dig_bytes, w.d_out.p, staged_b64, hipMemcpyDeviceToHost, w.stream) != hipSuccess))
         return DFS_E_HIP;
     cp.clear();  // direct: into the handlers' pinned buffers
-    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i) {
+    for (uint32_t i = static_cast<uint32_t>(pre.out); i < n; ++i) {
         const Req* r = batch[i];
         if (r->out_bytes)
             cp.push_back({reinterpret_cast<uint64_t>(w.d_out.as<char>() + b64_off[static_cast<uint64_t>(i) * N]),
@@ -304,14 +364,16 @@ int run_uploads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& 
         std::memcpy(r->fd, h + 32ull * i, 32);
         std::memcpy(r->frd, h + 32ull * n + 32ull * N * i, 32ull * N);
         // its Base64, [fragment] order (direct: already in place)
-        r->out_src = i < staged ? h + dig_bytes + b64_off[static_cast<uint64_t>(i) * N] : nullptr;
+        r->out_src = i < pre.out ? h + dig_bytes + b64_off[static_cast<uint64_t>(i) * N] : nullptr;
     }
+    grant_views(batch, res);
     return DFS_OK;
 }
 
 int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync& bs, Timing& tm) {
     const uint32_t n = static_cast<uint32_t>(batch.size()), N = B->nfrag;
-    const size_t staged = order_batch(batch);
+    const Prefix pre = order_batch(batch);
+    const size_t staged = pre.in;
     uint64_t staged_in = 0, staged_out = 0;
     const bool have_f = batch.front()->exp_frag != nullptr, have_i = batch.front()->exp_file != nullptr;
     std::vector<uint64_t> in_off(n), file_len(n), file_off(n);
@@ -336,12 +398,14 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
         file_len[i] = r->len;
         file_off[i] = out_total;
         out_total += (r->len + 15) & ~15ull;
-        if (i + 1 == staged) staged_in = total, staged_out = out_total;
+        if (i + 1 == pre.in) staged_in = total;
+        if (i + 1 == pre.out) staged_out = out_total;
         if (have_f) std::memcpy(ef.data() + 32ull * N * i, r->exp_frag, 32ull * N);
         if (have_i) std::memcpy(ei.data() + 32ull * i, r->exp_file, 32);
     }
+    dfs_view* res = w.next_out();
     int rc = w.pin_in.grow(staged_in + 16);
-    if (!rc) rc = w.pin_out.grow(staged_out + 16);
+    if (!rc) rc = res->pin.grow(staged_out + 16);
     if (!rc) rc = w.d_in.grow(total + 16);
     if (!rc) rc = w.d_out.grow(out_total + 16);
     if (rc) return rc;
@@ -371,10 +435,10 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
                             DFS_DEVICE_PTRS);
     if (rc != DFS_OK && rc != DFS_E_MISSING && rc != DFS_E_DECODE && rc != DFS_E_FRAG_MISMATCH && rc != DFS_E_CORRUPT)
         return rc;
-    if (staged_out && hipMemcpyAsync(w.pin_out.p, w.d_out.p, staged_out, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
+    if (staged_out && hipMemcpyAsync(res->pin.p, w.d_out.p, staged_out, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
         return DFS_E_HIP;
     cp.clear();  // direct, good files only (as the staged copy-out)
-    for (uint32_t i = static_cast<uint32_t>(staged); i < n; ++i)
+    for (uint32_t i = static_cast<uint32_t>(pre.out); i < n; ++i)
         if (st[i] == DFS_OK && batch[i]->len)
             cp.push_back({reinterpret_cast<uint64_t>(w.d_out.as<uint8_t>() + file_off[i]),
                           pinned_dev(batch[i]->out, batch[i]->len), batch[i]->len});
@@ -383,8 +447,9 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
     tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
         batch[i]->status = st[i];
-        batch[i]->out_src = i < staged ? w.pin_out.as<uint8_t>() + file_off[i] : nullptr;
+        batch[i]->out_src = i < pre.out ? res->pin.as<uint8_t>() + file_off[i] : nullptr;
     }
+    grant_views(batch, res);
     return DFS_OK;
 }
 
@@ -405,8 +470,9 @@ int run_reassembles(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSy
         spans[i] = dfs_span{total, batch[i]->len};
         total += (batch[i]->len + 15) & ~15ull;
     }
+    dfs_view* res = w.next_out();
     int rc = w.pin_in.grow(total + 16);
-    if (!rc) rc = w.pin_out.grow(32ull * n);
+    if (!rc) rc = res->pin.grow(32ull * n);
     if (!rc) rc = w.d_in.grow(total + 16);
     if (!rc) rc = w.d_dig.grow(32ull * n);
     if (rc) return rc;
@@ -416,13 +482,13 @@ int run_reassembles(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSy
         return DFS_E_HIP;
     rc = dfs_sha256_batch(w.ctx, w.d_in.as<uint8_t>(), spans.data(), n, w.d_dig.as<uint8_t>(), DFS_DEVICE_PTRS);
     if (rc) return rc;
-    if (hipMemcpyAsync(w.pin_out.p, w.d_dig.p, 32ull * n, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
+    if (hipMemcpyAsync(res->pin.p, w.d_dig.p, 32ull * n, hipMemcpyDeviceToHost, w.stream) != hipSuccess)
         return DFS_E_HIP;
     if (!wait_stream(w)) return DFS_E_HIP;
     tm.device = since(t_dev);
     for (uint32_t i = 0; i < n; ++i) {
         Req* r = batch[i];
-        const uint8_t* d = w.pin_out.as<uint8_t>() + 32ull * i;
+        const uint8_t* d = res->pin.as<uint8_t>() + 32ull * i;
         if (r->digest_out) std::memcpy(r->digest_out, d, 32);
         r->status = r->exp_file && std::memcmp(d, r->exp_file, 32) != 0 ? DFS_E_CORRUPT : DFS_OK;  // SN:455-458
         r->out_src = w.pin_in.as<uint8_t>() + in_off[i];  // the rebuilt file, where the handler assembled it
@@ -464,7 +530,7 @@ void worker_main(dfs_batcher* B, Worker* w) {
             ++B->st.batches;
             B->st.requests += batch.size();
             B->st.max_batch = std::max<uint64_t>(B->st.max_batch, batch.size());
-            for (const Req* r : batch) B->st.direct += r->direct;
+            for (const Req* r : batch) B->st.direct += r->direct, B->st.views += r->want_view;
             for (Req* r : batch) B->st.queue_s += std::chrono::duration<double>(now - r->arrive).count();
             if (!B->q.empty()) B->cv_work.notify_one();
         }
@@ -545,8 +611,15 @@ int submit(dfs_batcher* B, Req& r) {
     r.cv.wait(lk, [&] { return r.phase >= 3; });
     lk.unlock();
     const auto t_ready = Clock::now();
-    if (r.out_src && r.out_bytes && (r.kind == kUpload || r.status == DFS_OK))
+    if (r.want_view) {
+        // the view (and its reference) is the caller's only with a good result
+        const bool take = r.view && r.out_src && (r.kind == kUpload || r.status == DFS_OK);
+        *r.view_ptr = take ? r.out_src : nullptr;
+        *r.view_handle = take ? r.view : nullptr;
+        if (r.view && !take) (void)dfs_view_release(r.view);
+    } else if (r.out_src && r.out_bytes && (r.kind == kUpload || r.status == DFS_OK)) {
         std::memcpy(r.kind == kUpload ? static_cast<void*>(r.b64) : static_cast<void*>(r.out), r.out_src, r.out_bytes);
+    }
     const int status = r.status;
     std::lock_guard<std::mutex> bl(r.sync->mu);  // the last touch of the batch (the worker waits for it)
     r.sync->return_s += std::chrono::duration<double>(Clock::now() - t_ready).count();
@@ -606,7 +679,12 @@ int dfs_batcher_destroy(dfs_batcher* B) {
     for (Worker* w : B->workers) {
         if (w->th.joinable()) w->th.join();
         (void)hipSetDevice(B->device);
-        for (Buf* b : {&w->pin_in, &w->pin_out, &w->d_in, &w->d_out, &w->d_dig}) b->release();
+        for (dfs_view& v : w->outs) {  // views still out: their holders read this memory
+            std::unique_lock<std::mutex> lk(v.mu);
+            v.cv.wait(lk, [&] { return v.refs == 0; });
+            v.pin.release();
+        }
+        for (Buf* b : {&w->pin_in, &w->d_in, &w->d_out, &w->d_dig}) b->release();
         if (w->ctx) dfs_close(w->ctx);  // destroys its stream
         if (w->done) (void)hipEventDestroy(w->done);
         delete w;
@@ -655,8 +733,16 @@ int dfs_batcher_stats(dfs_batcher* B, dfs_batcher_stats_t* out) {
     return DFS_OK;
 }
 
-int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t* file_digest, uint8_t* frag_digest,
-                      char* b64, uint64_t b64_cap, uint64_t* b64_off) {
+}  // extern "C"
+
+namespace {
+
+// b64 != NULL: the Base64 is copied (or DMA'd) into the caller's buffer;
+// view_ptr != NULL: it is handed out as a view of the batch's result buffer.
+int submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t* file_digest, uint8_t* frag_digest,
+                  char* b64, uint64_t b64_cap, uint64_t* b64_off, const char** view_ptr, dfs_view** view) {
+    if (view_ptr) *view_ptr = nullptr;
+    if (view) *view = nullptr;
     if (!B || (len && !file) || !file_digest || !frag_digest || !b64_off) return DFS_E_ARG;
     if (len >= kMaxFile) return DFS_E_ARG;  // refused here, to this caller only: a batch fails as a whole
     const uint32_t N = B->nfrag;
@@ -664,7 +750,7 @@ int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t
     if (dfs_split_plan(len, N, fr) != DFS_OK) return DFS_E_ARG;
     b64_off[0] = 0;
     for (uint32_t i = 0; i < N; ++i) b64_off[i + 1] = b64_off[i] + enc_len(fr[i].len);  // SN:636
-    if (b64_off[N] > b64_cap || (b64_off[N] && !b64)) return DFS_E_ARG;
+    if (!view_ptr && (b64_off[N] > b64_cap || (b64_off[N] && !b64))) return DFS_E_ARG;
     Req r;
     r.kind = kUpload;
     r.file = file;
@@ -674,8 +760,34 @@ int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t
     r.frd = frag_digest;
     r.b64 = b64;
     r.b64_off = b64_off;
-    r.direct = in_pinned(file, len) && in_pinned(b64, r.out_bytes);
+    r.want_view = view_ptr != nullptr;
+    r.view_ptr = reinterpret_cast<const void**>(view_ptr);
+    r.view_handle = view;
+    r.direct = in_pinned(file, len) && (r.want_view || in_pinned(b64, r.out_bytes));
     return submit(B, r);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfs_submit_upload(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t* file_digest, uint8_t* frag_digest,
+                      char* b64, uint64_t b64_cap, uint64_t* b64_off) {
+    return submit_upload(B, file, len, file_digest, frag_digest, b64, b64_cap, b64_off, nullptr, nullptr);
+}
+
+int dfs_submit_upload_view(dfs_batcher* B, const uint8_t* file, uint64_t len, uint8_t* file_digest, uint8_t* frag_digest,
+                           const char** b64, uint64_t* b64_off, dfs_view** view) {
+    if (!b64 || !view) return DFS_E_ARG;
+    return submit_upload(B, file, len, file_digest, frag_digest, nullptr, 0, b64_off, b64, view);
+}
+
+int dfs_view_release(dfs_view* v) {
+    if (!v) return DFS_E_ARG;
+    std::lock_guard<std::mutex> lk(v->mu);
+    if (v->refs <= 0) return DFS_E_ARG;
+    if (--v->refs == 0) v->cv.notify_all();
+    return DFS_OK;
 }
 
 int dfs_submit_reassemble(dfs_batcher* B, const uint8_t* const* frags, const uint64_t* frag_len,
@@ -699,9 +811,16 @@ int dfs_submit_reassemble(dfs_batcher* B, const uint8_t* const* frags, const uin
     return submit(B, r);
 }
 
-int dfs_submit_download(dfs_batcher* B, const char* b64, const dfs_span* frags, uint64_t file_len,
-                        const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest, uint8_t* out) {
-    if (!B || !frags || (file_len && !out)) return DFS_E_ARG;
+}  // extern "C"
+
+namespace {
+
+int submit_download(dfs_batcher* B, const char* b64, const dfs_span* frags, uint64_t file_len,
+                    const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest, uint8_t* out,
+                    const uint8_t** view_ptr, dfs_view** view) {
+    if (view_ptr) *view_ptr = nullptr;
+    if (view) *view = nullptr;
+    if (!B || !frags || (file_len && !out && !view_ptr)) return DFS_E_ARG;
     Req r;
     r.kind = kDownload + (expected_frag_digest ? 2 : 0) + (expected_file_digest ? 1 : 0);
     // A request that could not run is refused here, to its caller only: inside
@@ -726,10 +845,29 @@ int dfs_submit_download(dfs_batcher* B, const char* b64, const dfs_span* frags, 
     r.exp_frag = expected_frag_digest;
     r.exp_file = expected_file_digest;
     r.out = out;
-    r.direct = in_pinned(out, file_len);
+    r.want_view = view_ptr != nullptr;
+    r.view_ptr = reinterpret_cast<const void**>(view_ptr);
+    r.view_handle = view;
+    r.direct = r.want_view || in_pinned(out, file_len);
     for (uint32_t k = 0; k < B->nfrag && r.direct; ++k)
         if (frags[k].len != DFS_SPAN_MISSING) r.direct = in_pinned(b64 + frags[k].off, frags[k].len);
     return submit(B, r);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dfs_submit_download(dfs_batcher* B, const char* b64, const dfs_span* frags, uint64_t file_len,
+                        const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest, uint8_t* out) {
+    return submit_download(B, b64, frags, file_len, expected_frag_digest, expected_file_digest, out, nullptr, nullptr);
+}
+
+int dfs_submit_download_view(dfs_batcher* B, const char* b64, const dfs_span* frags, uint64_t file_len,
+                             const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest,
+                             const uint8_t** out, dfs_view** view) {
+    if (!out || !view) return DFS_E_ARG;
+    return submit_download(B, b64, frags, file_len, expected_frag_digest, expected_file_digest, nullptr, out, view);
 }
 
 }  // extern "C"

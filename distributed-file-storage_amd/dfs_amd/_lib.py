@@ -59,7 +59,7 @@ class dfs_batcher_stats_t(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("max_batch", ctypes.c_uint64),
                 ("queue_s", ctypes.c_double), ("stage_in_s", ctypes.c_double), ("device_s", ctypes.c_double),
                 ("stage_out_s", ctypes.c_double), ("enqueue_s", ctypes.c_double), ("return_s", ctypes.c_double),
-                ("direct", ctypes.c_uint64)]
+                ("direct", ctypes.c_uint64), ("views", ctypes.c_uint64)]
 
 
 class dfs_batcher_opts(ctypes.Structure):
@@ -129,6 +129,9 @@ SIGNATURES = {
     "dfs_submit_upload": (_int, [_vp, _vp, _u64, _vp, _vp, _vp, _u64, _vp]),
     "dfs_submit_download": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "dfs_submit_reassemble": (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "dfs_submit_upload_view": (_int, [_vp, _vp, _u64, _vp, _vp, ctypes.POINTER(_vp), _vp, ctypes.POINTER(_vp)]),
+    "dfs_submit_download_view": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
+    "dfs_view_release": (_int, [_vp]),
     "dfs_comm_unique_id": (_int, [_vp]),
     "dfs_comm_init_rank": (_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_vp)]),
     "dfs_comm_init_all": (_int, [_vp, _u32, _vp]),

@@ -67,6 +67,50 @@ class Batcher:
         return (fd.tobytes(), [frd[i].tobytes() for i in range(self.nfrag)],
                 [b64[int(off[i]):int(off[i + 1])].tobytes() for i in range(self.nfrag)])
 
+    def upload_view(self, data: np.ndarray, keep: bool = False):
+        """dfs_submit_upload_view for one file (a uint8 array; read in place
+        when it lies in a PinnedBuffer): (fileId digest, fragment digests,
+        fragment Base64 strings), the Base64 copied out of the view, which is
+        then released.  keep=True returns (..., view handle) unreleased, for
+        tests of the buffer life cycle: give it to release_view."""
+        fd = np.zeros(32, np.uint8)
+        frd = np.zeros((self.nfrag, 32), np.uint8)
+        off = np.zeros(self.nfrag + 1, np.uint64)
+        ptr, view = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib().dfs_submit_upload_view(self._b, data.ctypes.data if data.size else None, data.size, fd.ctypes.data,
+                                           frd.ctypes.data, ctypes.byref(ptr), off.ctypes.data, ctypes.byref(view)),
+              "dfs_submit_upload_view")
+        total = int(off[self.nfrag])
+        text = ctypes.string_at(ptr.value, total) if total else b""
+        res = (fd.tobytes(), [frd[i].tobytes() for i in range(self.nfrag)],
+               [text[int(off[i]):int(off[i + 1])] for i in range(self.nfrag)])
+        if keep:
+            return res + (view,)
+        self.release_view(view)
+        return res
+
+    @staticmethod
+    def release_view(view) -> None:
+        if view:
+            check(lib().dfs_view_release(view), "dfs_view_release")
+
+    def download_view(self, text: np.ndarray, spans, file_len: int, ef: Optional[np.ndarray],
+                      ei: Optional[np.ndarray]) -> Tuple[int, Optional[bytes]]:
+        """dfs_submit_download_view: (status, the file's bytes copied out of
+        the view or None); the view is released."""
+        ptr, view = ctypes.c_void_p(), ctypes.c_void_p()
+        st = lib().dfs_submit_download_view(self._b, text.ctypes.data, spans, file_len,
+                                            ef.ctypes.data if ef is not None else None,
+                                            ei.ctypes.data if ei is not None else None, ctypes.byref(ptr),
+                                            ctypes.byref(view))
+        if st not in (L.DFS_OK, L.DFS_E_MISSING, L.DFS_E_DECODE, L.DFS_E_FRAG_MISMATCH, L.DFS_E_CORRUPT):
+            check(st, "dfs_submit_download_view")
+        out = None
+        if st == L.DFS_OK:
+            out = ctypes.string_at(ptr.value, file_len) if file_len else b""
+        self.release_view(view)
+        return st, out
+
     def download_into(self, text: np.ndarray, spans, file_len: int, ef: Optional[np.ndarray],
                       ei: Optional[np.ndarray], out: np.ndarray) -> int:
         """handleDownload's pipeline for one file from / into caller buffers:

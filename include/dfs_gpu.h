@@ -421,6 +421,7 @@ typedef struct dfs_batcher_stats_t {
     double enqueue_s;    /* handlers' time from the call to holding a queue slot */
     double return_s;     /* handlers' time from results ready to returning       */
     uint64_t direct;     /* requests moved straight from / to dfs_host_alloc buffers */
+    uint64_t views;      /* requests whose output was handed out as a view           */
 } dfs_batcher_stats_t;
 int dfs_batcher_stats(dfs_batcher* batcher, dfs_batcher_stats_t* stats);
 /* One upload (SN:127, 138-159, 636): file_digest[32], frag_digest[nfrag*32],
@@ -446,6 +447,28 @@ int dfs_submit_download(dfs_batcher* batcher, const char* b64, const dfs_span* f
  * untouched).  expected_file_digest may be NULL (not checked). */
 int dfs_submit_reassemble(dfs_batcher* batcher, const uint8_t* const* frags, const uint64_t* frag_len,
                           const uint8_t* expected_file_digest, uint8_t* out, uint8_t* file_digest_out);
+
+/* Outputs as views.  A handler does not need its own copy of the answer: it
+ * forwards the Base64 to the peers (sendFragmentsBulk, SN:226-246) or the file
+ * to the client (SN:460) and is done with it.  The *_view calls leave the
+ * output where the batch's single device-to-host DMA put it, in pinned memory
+ * the batcher owns, and return a pointer to it: no copy on the host and one
+ * DMA per batch instead of one per request (a pinned caller's per-request
+ * DMAs reach 36-40 GB/s on a link that moves 56 GB/s in one piece).  The
+ * input is read in place if it lies in a dfs_host_alloc buffer, else staged
+ * as for dfs_submit_upload.  *view is the handle to give back with
+ * dfs_view_release once the bytes have been used (NULL when the call failed
+ * or produced no view); a worker reuses a result buffer only after every view
+ * of it was released, so a handler that keeps one stalls that worker's
+ * second-next batch, and dfs_batcher_destroy waits for all of them.
+ * Same results and return codes as the calls above. */
+typedef struct dfs_view dfs_view;
+int dfs_submit_upload_view(dfs_batcher* batcher, const uint8_t* file, uint64_t len, uint8_t* file_digest,
+                           uint8_t* frag_digest, const char** b64, uint64_t* b64_off, dfs_view** view);
+int dfs_submit_download_view(dfs_batcher* batcher, const char* b64, const dfs_span* frags, uint64_t file_len,
+                             const uint8_t* expected_frag_digest, const uint8_t* expected_file_digest,
+                             const uint8_t** out, dfs_view** view);
+int dfs_view_release(dfs_view* view);
 
 /* ---- multi-GPU placement over RCCL / xGMI (SN:143-145, 195-259, 422-446) -- */
 /* One rank per GPU; node k (0-based) is hosted by rank k mod W (W = ranks).

@@ -203,3 +203,83 @@ def test_concurrent_raw_fragment_downloads_vs_oracle():
         _run_threads(48, work)
         s = b.stats()
         assert s["requests"] >= 48 * 3 * 2 and s["max_batch"] > 1
+
+
+def test_view_outputs_mixed_with_copies():
+    """dfs_submit_upload_view / dfs_submit_download_view: the answer stays in
+    the batch's pinned result buffer and the handler gets a pointer.  Handlers
+    asking for views (pinned or pageable inputs) share batches with handlers
+    that take copies; every result bit-exact vs the oracle; a failed download
+    hands out no view."""
+    from dfs_amd import _lib as L
+    from dfs_amd.batcher import PinnedBuffer
+    nfrag, threads, per = 5, 48, 3
+    with Batcher(0, nfrag, max_wait_us=3000) as b:
+        def work(t):
+            kind = t % 3  # 0: pinned input + views, 1: pageable input + views, 2: copies
+            for k in range(per):
+                i = t * per + k
+                data = _file(i)
+                n = len(data)
+                efd, efrd, eb64, eoff = O.c_upload_batch([data], nfrag)
+                if kind == 2:
+                    fd, frd, texts = b.upload(data)
+                else:
+                    pb = PinnedBuffer(max(n, 1)) if kind == 0 else None
+                    src = pb.array[:n] if pb else np.frombuffer(data, np.uint8).copy()
+                    if pb:
+                        src[:] = np.frombuffer(data, np.uint8)
+                    fd, frd, texts = b.upload_view(src)
+                    if pb:
+                        pb.free()
+                assert fd == efd[0].tobytes() and frd == [efrd[0, j].tobytes() for j in range(nfrag)], i
+                assert b"".join(texts) == eb64, i
+                if kind == 2:
+                    st, back = b.download(texts, n, frd, fd)
+                    assert st == 0 and back == data, (i, st)
+                    continue
+                total = len(eb64)
+                tb = PinnedBuffer(max(total, 1)) if kind == 0 else None
+                text = tb.array if tb else np.zeros(max(total, 1), np.uint8)
+                text[:total] = np.frombuffer(eb64, np.uint8)
+                spans = (L.dfs_span * nfrag)()
+                for j in range(nfrag):
+                    spans[j].off, spans[j].len = int(eoff[j]), int(eoff[j + 1] - eoff[j])
+                bad = k == 2 and n > 0
+                ei = np.frombuffer(bytes(32) if bad else fd, np.uint8)
+                st, back = b.download_view(text, spans, n, np.frombuffer(b"".join(frd), np.uint8), ei)
+                if bad:
+                    assert st == dfs_amd.DFS_E_CORRUPT and back is None, (i, st)
+                else:
+                    assert st == 0 and back == data, (i, st)
+                if tb:
+                    tb.free()
+        _run_threads(threads, work)
+        s = b.stats()
+        assert s["requests"] == 2 * threads * per
+        assert s["views"] == 2 * (threads // 3) * per * 2
+        assert s["batches"] < s["requests"]
+
+
+def test_view_kept_across_later_batches():
+    """A view stays readable while later batches run: each worker alternates
+    between two result buffers and takes one again only after every view of
+    it was released (one worker here, so batch 3 waits for batch 1's view)."""
+    import time
+    with Batcher(0, 5, max_wait_us=100, depth=1) as b:
+        d1, d2, d3 = (O.c_synth(900 + j, 0, 300000 + j) for j in range(3))
+        want1 = O.c_upload_batch([d1], 5)[2]
+        *_, texts1, view1 = b.upload_view(np.frombuffer(d1, np.uint8), keep=True)
+        assert b"".join(texts1) == want1
+        fd2, _, texts2 = b.upload_view(np.frombuffer(d2, np.uint8))  # the other buffer
+        assert b"".join(texts2) == O.c_upload_batch([d2], 5)[2]
+        done = []
+        th = threading.Thread(target=lambda: done.append(b.upload_view(np.frombuffer(d3, np.uint8))))
+        th.start()
+        time.sleep(0.5)
+        assert not done  # the third batch needs the first buffer back
+        Batcher.release_view(view1)
+        th.join(timeout=60)
+        assert done and b"".join(done[0][2]) == O.c_upload_batch([d3], 5)[2]
+        from dfs_amd import _lib as L
+        assert L.lib().dfs_view_release(view1) == dfs_amd.DFS_E_ARG  # nothing left to release

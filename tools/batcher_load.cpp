@@ -9,7 +9,9 @@
 //
 //   batcher_load <clients> <seconds> <upload|download> <file_bytes> <nfrag> [max_wait_us] [depth] [pinned]
 // pinned = 1: every client's buffers come from dfs_host_alloc (direct
-// requests: DMA straight from / into them, no staging copies).
+// requests: DMA straight from / into them, no staging copies); pinned = 2:
+// pinned inputs and the outputs as views (dfs_submit_*_view: the answer stays
+// in the batch's result buffer, one DMA per batch, released after the check).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -131,7 +133,8 @@ int main(int argc, char** argv) {
     dfs_batcher_opts o{};
     if (argc > 6) o.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
     if (argc > 7) o.depth = static_cast<uint32_t>(std::atoi(argv[7]));
-    const bool pinned = argc > 8 && std::atoi(argv[8]) != 0;
+    const int pin_mode = argc > 8 ? std::atoi(argv[8]) : 0;
+    const bool pinned = pin_mode != 0, views = pin_mode == 2;
     // A client buffer: pageable (std::vector) or a slice of one dfs_host_alloc
     // pool (a server would pin its connection buffers once, not per request;
     // one pool instead of 3 x C pinned allocations also keeps the setup of
@@ -231,9 +234,17 @@ int main(int argc, char** argv) {
                 const auto t0 = Clock::now();
                 const double k0 = thread_cpu_now();
                 int rc;
-                if (up) {
+                const char* ans_b64 = reinterpret_cast<const char*>(mb.data());
+                const uint8_t* ans_file = out.data();
+                dfs_view* view = nullptr;
+                if (up && views) {
+                    rc = dfs_submit_upload_view(B, in.data(), S, mfd.data(), mfrd.data(), &ans_b64, moff.data(), &view);
+                } else if (up) {
                     rc = dfs_submit_upload(B, in.data(), S, mfd.data(), mfrd.data(), reinterpret_cast<char*>(mb.data()), cap,
                                            moff.data());
+                } else if (views) {
+                    rc = dfs_submit_download_view(B, reinterpret_cast<const char*>(text[f].data()), spans.data(), S,
+                                                  frd[f].data(), fd[f].data(), &ans_file, &view);
                 } else {
                     rc = dfs_submit_download(B, reinterpret_cast<const char*>(text[f].data()), spans.data(), S, frd[f].data(),
                                              fd[f].data(), out.data());
@@ -248,10 +259,11 @@ int main(int argc, char** argv) {
                     first_rc.compare_exchange_strong(z, rc);
                 } else if (it % 8) {  // every 8th result is compared in full (the handler's own work stays small)
                 } else if (up && (std::memcmp(mfd.data(), fd[f].data(), 32) || std::memcmp(mfrd.data(), frd[f].data(), 32 * N) ||
-                                std::memcmp(mb.data(), b64[f].data(), off[f][N])))
+                                std::memcmp(ans_b64, b64[f].data(), off[f][N])))
                     bad = true, ++mismatches;
-                else if (!up && std::memcmp(out.data(), file[f].data(), S))
+                else if (!up && std::memcmp(ans_file, file[f].data(), S))
                     bad = true, ++mismatches;
+                if (view) dfs_view_release(view);
                 if (t0 >= measure_from) cpu_out[t] += thread_cpu_now() - k1;
                 if (t1 >= deadline) break;
             }
@@ -291,6 +303,7 @@ int main(int argc, char** argv) {
     st.batches -= st_warm.batches;
     st.requests -= st_warm.requests;
     st.direct -= st_warm.direct;
+    st.views -= st_warm.views;
     st.queue_s -= st_warm.queue_s;
     st.stage_in_s -= st_warm.stage_in_s;
     st.device_s -= st_warm.device_s;
@@ -300,11 +313,11 @@ int main(int argc, char** argv) {
     dfs_batcher_destroy(B);
     std::printf("{\"clients\": %d, \"kind\": \"%s\", \"requests\": %zu, \"wall_s\": %.4f, \"gbps\": %.4f, "
                 "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"cpu_s\": %.3f, \"throttled_s\": %.3f, \"cpu_threads_s\": {\"clients\": %.3f, \"workers\": %.3f, \"other\": %.3f}, \"client_cpu_us_per_req\": {\"in_submit\": %.1f, \"outside\": %.1f}, \"ok\": %s, \"file0_id\": \"%s\", \"file1_id\": \"%s\", "
-                "\"pinned\": %d, \"stats\": {\"direct\": %llu, \"batches\": %llu, \"requests\": %llu, \"max_batch\": %llu, \"queue_s\": %.4f, "
+                "\"pinned\": %d, \"stats\": {\"direct\": %llu, \"views\": %llu, \"batches\": %llu, \"requests\": %llu, \"max_batch\": %llu, \"queue_s\": %.4f, "
                 "\"stage_in_s\": %.4f, \"device_s\": %.4f, \"stage_out_s\": %.4f, \"enqueue_s\": %.4f, \"return_s\": %.4f}}\n",
                 C, up ? "upload" : "download", all.size(), wall, all.size() * static_cast<double>(S) / wall / 1e9,
                 pct(0.5) * 1e3, pct(0.99) * 1e3, (u1 - u0) / 1e6, (th1 - th0) / 1e6, cpu_cl, cpu_wk, cpu_ot, cin / std::max<size_t>(all.size(), 1) * 1e6, cout_ / std::max<size_t>(all.size(), 1) * 1e6, bad ? "false" : "true", hex(fd[0].data()).c_str(),
-                hex(fd[1].data()).c_str(), pinned ? 1 : 0, (unsigned long long)st.direct, (unsigned long long)st.batches, (unsigned long long)st.requests,
+                hex(fd[1].data()).c_str(), pin_mode, (unsigned long long)st.direct, (unsigned long long)st.views, (unsigned long long)st.batches, (unsigned long long)st.requests,
                 (unsigned long long)st.max_batch, st.queue_s, st.stage_in_s, st.device_s, st.stage_out_s, st.enqueue_s,
                 st.return_s);
     if (bad)
