@@ -44,6 +44,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <shared_mutex>
@@ -193,16 +194,42 @@ struct Worker {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // polled with sleeps (dfs::quiet_wait): the worker does not spin on the CPU share
     Buf pin_in, d_in, d_out, d_dig;
-    dfs_view outs[2];  // result buffers, alternating: batch k's views may outlive batch k + 1
-    int out_i = 0;
+    // Result buffers, taken in turn: batch k's views may outlive batch k + 1.
+    // Two in the steady state.  Handlers that keep views while they wait for
+    // a later request of their own could otherwise stop the worker for good
+    // (it would wait for their views, they for its next batch), so a buffer
+    // that stays referenced for kViewPatience makes the worker add another,
+    // up to kMaxOuts; only there does it wait without a limit.
+    static constexpr size_t kMaxOuts = 8;
+    static constexpr std::chrono::milliseconds kViewPatience{20};
+    std::vector<std::unique_ptr<dfs_view>> outs;
+    size_t out_i = 0;
     std::thread th;
-    Worker() { pin_in.pinned = true; }
-    // The result buffer of the next batch, once no view of it is left.
+    Worker() {
+        pin_in.pinned = true;
+        for (int i = 0; i < 2; ++i) outs.emplace_back(new dfs_view);
+    }
+    // The result buffer of the next batch: one without views.
     dfs_view* next_out() {
-        dfs_view* v = &outs[out_i ^= 1];
+        for (size_t k = 1; k <= outs.size(); ++k) {
+            dfs_view* v = outs[(out_i + k) % outs.size()].get();
+            std::lock_guard<std::mutex> lk(v->mu);
+            if (v->refs == 0) {
+                out_i = (out_i + k) % outs.size();
+                return v;
+            }
+        }
+        dfs_view* v = outs[out_i = (out_i + 1) % outs.size()].get();  // the oldest
         std::unique_lock<std::mutex> lk(v->mu);
-        v->cv.wait(lk, [&] { return v->refs == 0; });
-        return v;
+        if (outs.size() >= kMaxOuts) {
+            v->cv.wait(lk, [&] { return v->refs == 0; });
+            return v;
+        }
+        if (v->cv.wait_for(lk, kViewPatience, [&] { return v->refs == 0; })) return v;
+        lk.unlock();
+        outs.emplace_back(new dfs_view);
+        out_i = outs.size() - 1;
+        return outs.back().get();
     }
 };
 
@@ -679,10 +706,10 @@ int dfs_batcher_destroy(dfs_batcher* B) {
     for (Worker* w : B->workers) {
         if (w->th.joinable()) w->th.join();
         (void)hipSetDevice(B->device);
-        for (dfs_view& v : w->outs) {  // views still out: their holders read this memory
-            std::unique_lock<std::mutex> lk(v.mu);
-            v.cv.wait(lk, [&] { return v.refs == 0; });
-            v.pin.release();
+        for (auto& v : w->outs) {  // views still out: their holders read this memory
+            std::unique_lock<std::mutex> lk(v->mu);
+            v->cv.wait(lk, [&] { return v->refs == 0; });
+            v->pin.release();
         }
         for (Buf* b : {&w->pin_in, &w->d_in, &w->d_out, &w->d_dig}) b->release();
         if (w->ctx) dfs_close(w->ctx);  // destroys its stream

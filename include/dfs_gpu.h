@@ -458,9 +458,10 @@ int dfs_submit_reassemble(dfs_batcher* batcher, const uint8_t* const* frags, con
  * input is read in place if it lies in a dfs_host_alloc buffer, else staged
  * as for dfs_submit_upload.  *view is the handle to give back with
  * dfs_view_release once the bytes have been used (NULL when the call failed
- * or produced no view); a worker reuses a result buffer only after every view
- * of it was released, so a handler that keeps one stalls that worker's
- * second-next batch, and dfs_batcher_destroy waits for all of them.
+ * or produced no view).  A worker reuses a result buffer only after every
+ * view of it was released and dfs_batcher_destroy waits for all of them, so
+ * release promptly, and before the same thread submits again: a worker that
+ * finds its buffers still referenced adds more (up to 8), then waits.
  * Same results and return codes as the calls above. */
 typedef struct dfs_view dfs_view;
 int dfs_submit_upload_view(dfs_batcher* batcher, const uint8_t* file, uint64_t len, uint8_t* file_digest,
