@@ -229,11 +229,13 @@ public:
         std::vector<uint64_t> off(parts + 1);
         std::vector<dfs_span> split(parts);
         check(dfs_split_plan(file.size(), parts, split.data()), "split");
-        uint64_t cap = 0;
-        for (auto& s : split) cap += dfs_b64_encoded_len(s.len);
-        std::string b64(cap, '\0');
-        check(dfs_submit_upload(b, file.empty() ? nullptr : file.data(), file.size(), fd.data(), frd.data(),
-                                cap ? &b64[0] : nullptr, cap, off.data()),
+        // The Base64 is only forwarded (into the fragments' strings here, into
+        // the storeFragments bodies in the reference, SN:226-246): take it as
+        // a view of the batch's result buffer and give the view back at once.
+        const char* b64 = nullptr;
+        dfs_view* view = nullptr;
+        check(dfs_submit_upload_view(b, file.empty() ? nullptr : file.data(), file.size(), fd.data(), frd.data(), &b64,
+                                     off.data(), &view),
               "handleUpload");
         std::vector<Fragment> frags;
         for (int i = 0; i < parts; ++i) {
@@ -241,9 +243,10 @@ public:
             f.index = i;
             f.data.assign(file.begin() + split[i].off, file.begin() + split[i].off + split[i].len);
             f.hash = hex(frd.data() + 32 * i);
-            f.b64 = b64.substr(off[i], off[i + 1] - off[i]);
+            f.b64.assign(b64 + off[i], off[i + 1] - off[i]);
             frags.push_back(std::move(f));
         }
+        check(dfs_view_release(view), "dfs_view_release");
         return {hex(fd.data()), std::move(frags)};
     }
 

@@ -262,24 +262,26 @@ def test_view_outputs_mixed_with_copies():
 
 
 def test_view_kept_across_later_batches():
-    """A view stays readable while later batches run: each worker alternates
-    between two result buffers and takes one again only after every view of
-    it was released (one worker here, so batch 3 waits for batch 1's view)."""
-    import time
+    """A view stays readable and unchanged while later batches run: a worker
+    takes a result buffer again only after every view of it was released, and
+    adds a buffer rather than wait for a handler that keeps its view (one
+    worker here: the third batch would need the first batch's buffer)."""
+    from dfs_amd import _lib as L
     with Batcher(0, 5, max_wait_us=100, depth=1) as b:
         d1, d2, d3 = (O.c_synth(900 + j, 0, 300000 + j) for j in range(3))
         want1 = O.c_upload_batch([d1], 5)[2]
-        *_, texts1, view1 = b.upload_view(np.frombuffer(d1, np.uint8), keep=True)
-        assert b"".join(texts1) == want1
-        fd2, _, texts2 = b.upload_view(np.frombuffer(d2, np.uint8))  # the other buffer
-        assert b"".join(texts2) == O.c_upload_batch([d2], 5)[2]
-        done = []
-        th = threading.Thread(target=lambda: done.append(b.upload_view(np.frombuffer(d3, np.uint8))))
-        th.start()
-        time.sleep(0.5)
-        assert not done  # the third batch needs the first buffer back
-        Batcher.release_view(view1)
-        th.join(timeout=60)
-        assert done and b"".join(done[0][2]) == O.c_upload_batch([d3], 5)[2]
-        from dfs_amd import _lib as L
+        fd1, frd1, off1 = np.zeros(32, np.uint8), np.zeros((5, 32), np.uint8), np.zeros(6, np.uint64)
+        import ctypes
+        ptr, view1 = ctypes.c_void_p(), ctypes.c_void_p()
+        a1 = np.frombuffer(d1, np.uint8)
+        assert L.lib().dfs_submit_upload_view(b._b, a1.ctypes.data, a1.size, fd1.ctypes.data, frd1.ctypes.data,
+                                              ctypes.byref(ptr), off1.ctypes.data, ctypes.byref(view1)) == 0
+        try:
+            assert ctypes.string_at(ptr.value, int(off1[5])) == want1
+            for d in (d2, d3, d2, d3):  # later batches, through the other buffer(s)
+                _, _, texts = b.upload_view(np.frombuffer(d, np.uint8))
+                assert b"".join(texts) == O.c_upload_batch([d], 5)[2]
+            assert ctypes.string_at(ptr.value, int(off1[5])) == want1  # still there, untouched
+        finally:
+            Batcher.release_view(view1)
         assert L.lib().dfs_view_release(view1) == dfs_amd.DFS_E_ARG  # nothing left to release
