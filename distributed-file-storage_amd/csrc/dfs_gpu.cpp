@@ -151,6 +151,15 @@ hipError_t d2h(dfs_ctx* c, void* dst, const void* src, size_t n, hipStream_t s) 
     return e;
 }
 int ctx_device(dfs_ctx* c) { return c->device; }
+// The ctx's second stream (created on first use), for a stream kernel that
+// runs beside the SHA kernel of the same call.
+hipError_t ctx_aux_stream(dfs_ctx* c, hipStream_t* aux) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess && !c->aux) e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+    *aux = c->aux;
+    return e;
+}
 std::mutex& ctx_store_mutex(dfs_ctx* c) { return c->store_mu; }
 StoreStaging*& ctx_store(dfs_ctx* c) { return c->store; }
 }  // namespace dfs

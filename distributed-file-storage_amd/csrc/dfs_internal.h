@@ -256,6 +256,7 @@ struct CopySpan {
 };
 int copy_spans(dfs_ctx* c, const CopySpan* spans, size_t n);
 int ctx_device(dfs_ctx* c);
+hipError_t ctx_aux_stream(dfs_ctx* c, hipStream_t* aux);  // the ctx's second stream, created on first use
 std::mutex& ctx_store_mutex(dfs_ctx* c);  // guards the staging ring only
 StoreStaging*& ctx_store(dfs_ctx* c);
 

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -39,11 +40,22 @@ struct dfs_replica_plan {
     std::vector<dfs_held_frag> frags; // held order
     uint64_t held_bytes = 0, raw_bytes = 0;
     dfs::Plan dig_plan;               // the placement schedule over 32-byte digests
+    // The check can run in slices of the held order (DFS_REPLICA_SLICES; one
+    // by default): slice i is hashed while slice i + 1 is decoded beside it
+    // on the ctx's second stream.  Each slice has its own decode job table (with its
+    // tile prefix and sentinel) inside d_jobs and its own length-sorted lanes
+    // inside d_desc; status and digest slots stay indexed by held fragment.
+    struct Slice {
+        uint64_t k0 = 0, k1 = 0;   // held fragments [k0, k1)
+        uint64_t job0 = 0;         // first entry of its job table in d_jobs
+        uint64_t ntiles = 0;
+        uint32_t prio = 0;         // lanes of its long items (sort_sha_lanes)
+    };
+    std::vector<Slice> slices;
+    std::vector<hipEvent_t> ev;       // [0]: the call's start on its stream; [i]: slice i decoded
     // device tables
     StreamJob* d_jobs = nullptr;
-    uint64_t ntiles = 0;
     ShaDesc* d_desc = nullptr;
-    uint32_t prio = 0;
     uint32_t* d_queue = nullptr;
     int32_t* d_status = nullptr;      // decode status per held fragment
     uint8_t* d_got = nullptr;         // digests of the decoded fragments
@@ -145,6 +157,8 @@ int build_layout(uint32_t W, uint32_t me, uint32_t N, const uint32_t* nfiles, co
 void free_plan(dfs_replica_plan* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
+    for (hipEvent_t e : p->ev)
+        if (e) (void)hipEventDestroy(e);
     for (void* q : {static_cast<void*>(p->d_jobs), static_cast<void*>(p->d_desc), static_cast<void*>(p->d_queue),
                     static_cast<void*>(p->d_status), static_cast<void*>(p->d_got), static_cast<void*>(p->d_expected),
                     static_cast<void*>(p->d_dig_t), static_cast<void*>(p->d_piece_start),
@@ -247,27 +261,50 @@ int dfs_replica_plan_create(dfs_comm* const* comms, uint32_t ncomms, uint32_t nf
             if (!rc && p->dig_plan.dst_off[nfrag] != 32 * K) rc = DFS_E_ARG;  // held order == schedule order
             // decode jobs into the raw buffer (raw_off is 16-byte aligned: no
             // head bytes as long as d_raw is) and SHA lanes over the raw bytes
-            std::vector<StreamJob> jobs(K);
-            std::vector<uint64_t> items(K);
+            // One slice unless DFS_REPLICA_SLICES asks for more: measured on the
+            // 131,072 x 256 KiB / N = 8 shard (524,288 held fragments per call),
+            // two slices make the check slower (38.9 against 36.0 ms) — the
+            // narrow decode beside the SHA waves costs the SHA kernel more
+            // clock than the overlap saves.
+            uint64_t nslices = 1;
+            if (const char* e = std::getenv("DFS_REPLICA_SLICES"))
+                nslices = std::min<uint64_t>(std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)), std::max<uint64_t>(K, 1));
+            nslices = std::min<uint64_t>(nslices, 16);
+            std::vector<StreamJob> jobs;   // the slices' job tables, back to back
             std::vector<ShaDesc> desc(K);
-            for (uint64_t k = 0; k < K && !rc; ++k) {
-                const dfs_held_frag& h = L.frags[k];
-                StreamJob& j = jobs[k];
-                j = StreamJob{};
-                j.src_off = h.b64_off;
-                j.len = h.b64_len;
-                j.dst_off = h.raw_off;
-                j.expect = h.raw_len + 1;
-                j.id = static_cast<uint32_t>(k);
-                items[k] = dfs::decode_items(h.b64_len, static_cast<uintptr_t>(h.raw_off));
-                desc[k] = ShaDesc{h.raw_off, h.raw_len, h.raw_len, static_cast<uint32_t>(k), 0, 0};
-                if (h.raw_len >= (1ull << 37)) rc = DFS_E_ARG;
+            for (uint64_t i = 0; i < nslices && !rc; ++i) {
+                dfs_replica_plan::Slice sl;
+                sl.k0 = K * i / nslices;
+                sl.k1 = K * (i + 1) / nslices;
+                std::vector<StreamJob> js(sl.k1 - sl.k0);
+                std::vector<uint64_t> items(js.size());
+                for (uint64_t k = sl.k0; k < sl.k1 && !rc; ++k) {
+                    const dfs_held_frag& h = L.frags[k];
+                    StreamJob& j = js[k - sl.k0];
+                    j = StreamJob{};
+                    j.src_off = h.b64_off;
+                    j.len = h.b64_len;
+                    j.dst_off = h.raw_off;
+                    j.expect = h.raw_len + 1;
+                    j.id = static_cast<uint32_t>(k);
+                    items[k - sl.k0] = dfs::decode_items(h.b64_len, static_cast<uintptr_t>(h.raw_off));
+                    desc[k] = ShaDesc{h.raw_off, h.raw_len, h.raw_len, static_cast<uint32_t>(k), 0, 0};
+                    if (h.raw_len >= (1ull << 37)) rc = DFS_E_ARG;
+                }
+                sl.ntiles = dfs::finish_stream_jobs(js, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
+                std::vector<ShaDesc> lanes(desc.begin() + sl.k0, desc.begin() + sl.k1);
+                sl.prio = dfs::sort_sha_lanes(lanes);
+                std::copy(lanes.begin(), lanes.end(), desc.begin() + sl.k0);
+                sl.job0 = jobs.size();
+                jobs.insert(jobs.end(), js.begin(), js.end());  // with its sentinel
+                p->slices.push_back(sl);
             }
             if (!rc) {
-                p->ntiles = dfs::finish_stream_jobs(jobs, items, static_cast<uint64_t>(dfs::kDecGpl) * dfs::kStreamBlock);
-                p->prio = dfs::sort_sha_lanes(desc);
                 p->frags = std::move(L.frags);
                 hipError_t e = hipSetDevice(p->device);
+                p->ev.assign(p->slices.size(), nullptr);
+                for (size_t i = 0; i < p->ev.size() && e == hipSuccess && p->ev.size() > 1; ++i)
+                    e = hipEventCreateWithFlags(&p->ev[i], hipEventDisableTiming);
                 if (e == hipSuccess) e = dev_copy(&p->d_jobs, jobs);
                 if (e == hipSuccess) e = dev_copy(&p->d_desc, desc);
                 if (e == hipSuccess) e = dev_copy(&p->d_piece_start, L.piece_start);
@@ -355,10 +392,36 @@ int dfs_replica_check(dfs_ctx* ctx, dfs_replica_plan* p, const char* d_held, uin
     HIPR(dfs::launch_fill_u32(d_failed, p->W, 0u, s));
     if (!K) return DFS_OK;
     HIPR(dfs::launch_fill_u32(reinterpret_cast<uint32_t*>(p->d_status), K, 0u, s));
-    HIPR(dfs::launch_b64_decode(d_held, p->d_jobs, static_cast<uint32_t>(K), p->ntiles, d_raw, p->d_status, nullptr,
-                                s));
-    HIPR(dfs::launch_sha256(d_raw, p->d_desc, static_cast<uint32_t>(K), static_cast<uint32_t>(K), p->prio, p->d_got,
-                            p->d_got, p->d_queue, 4, s));
+    // Slice 0 is decoded at full width on the call's stream; slices 1.. on the
+    // ctx's second stream with a narrow, prioritised grid, each beside the
+    // hashing of the slice before it.  Nothing waits inside a kernel: a decode
+    // that finds no room beside the SHA waves simply runs after them.
+    const size_t ns = p->slices.size();
+    hipStream_t a = s;
+    if (ns > 1) {
+        HIPR(dfs::ctx_aux_stream(ctx, &a));
+        HIPR(hipEventRecord(p->ev[0], s));
+        HIPR(hipStreamWaitEvent(a, p->ev[0], 0));
+    }
+    for (size_t i = 0; i < ns; ++i) {
+        const dfs_replica_plan::Slice& sl = p->slices[i];
+        const uint32_t n = static_cast<uint32_t>(sl.k1 - sl.k0);
+        if (!n) continue;
+        if (i == 0)
+            HIPR(dfs::launch_b64_decode(d_held, p->d_jobs + sl.job0, n, sl.ntiles, d_raw, p->d_status, nullptr, s));
+        else {
+            HIPR(dfs::launch_b64_decode(d_held, p->d_jobs + sl.job0, n, sl.ntiles, d_raw, p->d_status, nullptr, a, 1u, 2u));
+            HIPR(hipEventRecord(p->ev[i], a));
+        }
+    }
+    for (size_t i = 0; i < ns; ++i) {
+        const dfs_replica_plan::Slice& sl = p->slices[i];
+        const uint32_t n = static_cast<uint32_t>(sl.k1 - sl.k0);
+        if (!n) continue;
+        if (i) HIPR(hipStreamWaitEvent(s, p->ev[i], 0));
+        HIPR(dfs::launch_sha256(d_raw, p->d_desc + sl.k0, n, static_cast<uint32_t>(K), sl.prio, p->d_got, p->d_got,
+                                p->d_queue, ns > 1 ? 3 : 4, s));
+    }
     HIPR(dfs::launch_replica_verdict(p->d_status, p->d_got, p->d_expected, K, p->d_piece_start, p->d_piece_rank,
                                      p->npieces, DFS_E_DECODE, DFS_E_FRAG_MISMATCH, d_verdict, d_failed, s));
     return DFS_OK;

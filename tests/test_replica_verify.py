@@ -42,9 +42,15 @@ def _run(engine, lens, nfrag, align128, seed):
                 host=files.cpu().numpy(), offs=offs)
 
 
+@pytest.mark.parametrize("slices", [0, 3])
 @pytest.mark.parametrize("align128", [False, True])
 @pytest.mark.parametrize("shape", ["ragged", "uniform-large"])
-def test_replica_verify_single_rank(engine, align128, shape):
+def test_replica_verify_single_rank(engine, align128, shape, slices, monkeypatch):
+    """slices = 3: the check in three slices (DFS_REPLICA_SLICES; one by
+    default), slice i hashed while slice i + 1 is decoded on the second
+    stream."""
+    if slices:
+        monkeypatch.setenv("DFS_REPLICA_SLICES", str(slices))
     rng = np.random.default_rng(5 + align128)
     nfrag = 5 if shape == "ragged" else 8
     if shape == "ragged":
@@ -64,7 +70,7 @@ def test_replica_verify_single_rank(engine, align128, shape):
         raw = torch.zeros(rp.raw_bytes + 16, dtype=torch.uint8, device=dev)
         verdict = torch.full((rp.nheld,), 99, dtype=torch.int32, device=dev)
         failed = torch.full((1,), 99, dtype=torch.int32, device=dev)
-        print(f"replica verify {shape} align128={align128}: {rp.nheld} held fragments", flush=True)
+        print(f"replica verify {shape} align128={align128} slices={slices}: {rp.nheld} held fragments", flush=True)
         rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
         torch.cuda.synchronize()
         assert int(failed[0]) == 0 and bool((verdict == 0).all())
