@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 GPU check: parity tests, smoke, default bench (N=1).
+# GPU check: parity tests, smoke, default bench (N=1).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 evidence after twin lanes + decode-ahead download: rocprofv3 kernel
+# Evidence after twin lanes + decode-ahead download: rocprofv3 kernel
 # traces and PMC passes (scripts/profile.sh), the default bench line (all
 # legs), SHA alone (--mode serial), and the N>1 step on one rank at 4 and 2
 # chunks (--placement-step).  Stops at the first failing step.

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 (late) check: parity tests, smoke, default bench, then the SHA
+# GPU check: parity tests, smoke, default bench, then the SHA
 # memory-footprint probe beside Base64 (files aliased onto 1 vs 65,536).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

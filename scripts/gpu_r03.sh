@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU check: parity tests, the allocation-free entry's test, smoke,
+# GPU check: parity tests, the allocation-free entry's test, smoke,
 # then (unless NO_BENCH) the default bench (N=1).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

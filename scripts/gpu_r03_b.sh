@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 check B: GPU tests, default bench without the batcher leg, the
+# GPU check B: GPU tests, default bench without the batcher leg, the
 # fused-upload mode on today's tree, the N > 1 step on one rank.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 record: GPU tests, smoke, default bench (N=1), configs[2] shard on
+# Record run: GPU tests, smoke, default bench (N=1), configs[2] shard on
 # one GPU, configs[3] (256 MiB skew), the N > 1 step on one rank.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 rocprofv3 evidence: the round's profile.sh (kernel trace + PMC of
+# rocprofv3 evidence: scripts/profile.sh (kernel trace + PMC of
 # the headline bench and the download leg), then a kernel trace of the N > 1
 # step on one rank (upload + placement + holders' verify).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
