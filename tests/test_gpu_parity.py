@@ -63,6 +63,41 @@ def test_b64_encode_rfc_and_edges(engine, golden):
         assert g == O.c_b64_encode(m)
 
 
+def test_b64_encode_every_source_and_destination_phase(engine):
+    """Messages packed back to back: the source of a message starts at any
+    byte phase mod 4 and its Base64 at any dword phase mod 16 (0, 4, 8, 12).
+    Every one of the 16 combinations is steered to (a short filler message
+    before it) for each length: one partial group, a wave, a tile of 12 KiB
+    more or less a group, several tiles — so a lane's 16 chars straddle
+    16-byte chunks inside waves, across waves, across tiles and at a
+    message's last group.  Against Python's base64."""
+    rng = random.Random(77)
+    msgs, want = [], []
+    s = o = 0  # source bytes / Base64 chars before the next message
+
+    def add(m):
+        nonlocal s, o
+        msgs.append(m)
+        s += len(m)
+        o += 4 * ((len(m) + 2) // 3)
+
+    for n in [5, 13, 767, 769, 12287, 12288, 12289, 12301, 24576 + 7, 40001, 100003]:
+        for sp in range(4):
+            for dp in (0, 4, 8, 12):
+                # one or two fillers reach every phase (one alone reaches 12 of the 16)
+                fill = next((a, b) for a in range(1, 14) for b in range(0, 14)
+                            if (s + a + b) % 4 == sp and (o + 4 * ((a + 2) // 3) + 4 * ((b + 2) // 3)) % 16 == dp)
+                for k in fill:
+                    if k:
+                        add(rng.randbytes(k))
+                want.append((n, sp, dp, len(msgs)))
+                assert (s % 4, o % 16) == (sp, dp)
+                add(rng.randbytes(n))
+    got = engine.b64_encode(msgs)
+    for k, m in enumerate(msgs):
+        assert got[k] == base64.b64encode(m), (k, len(m), [w for w in want if w[3] == k])
+
+
 def test_b64_decode_jdk_cases(engine, golden):
     cases = golden["b64_decode_jdk"]
     got = engine.b64_decode([bytes.fromhex(d["input_hex"]) for d in cases])
