@@ -107,6 +107,10 @@ def parse(argv=None):
                          "fragment digest, and every fragment's Base64 through its SHA-256 (outside the timed region)")
     ap.add_argument("--placement", choices=("star", "ring"), default="star",
                     help="N>1: placement inside the timed step (the other one is timed beside it)")
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="N > 1 transport: RCCL over xGMI (one rank per GPU), or 'host': the library's host-staged "
+                         "communicator (shared-memory mailboxes, synchronous) with rank r on GPU r mod <GPUs present> "
+                         "- a functional rehearsal of the N > 1 step on fewer GPUs than ranks, never a measurement")
     ap.add_argument("--chunks", type=int, default=2,
                     help="N>1: file chunks pipelined through compute + placement (2: 65,536-file launches keep the "
                          "SHA twin lanes; chunk c of step k+1 waits only for chunk c's placement of step k)")
@@ -802,6 +806,8 @@ def multi_gpu(args, world, rank, local, log):
     from dfs_amd import placement as P
     from dfs_amd.engine import download_device
     dev = torch.device("cuda", local)
+    # the harness's own collectives: device tensors over nccl, host tensors over gloo (--comm host)
+    hdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
     F, S, N = args.files, args.file_size, args.nfrag
     eng = dfs_amd.FragmentEngine(local)   # compute ctx
     eng_c = dfs_amd.FragmentEngine(local)  # comm ctx (RCCL on its own stream)
@@ -890,7 +896,7 @@ def multi_gpu(args, world, rank, local, log):
             fn()
         torch.cuda.synchronize(dev)
         dist.barrier()
-        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=hdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item()) / reps
 
@@ -910,7 +916,7 @@ def multi_gpu(args, world, rank, local, log):
     # of one held fragment (to another alphabet char), every rank re-runs the
     # verify, then the placement restores the held buffer.
     ch0 = sh.chunks[0]
-    probe = torch.zeros(2, dtype=torch.int64, device=dev)
+    probe = torch.zeros(2, dtype=torch.int64, device=hdev)
     if rank == 0 and ch0["rp"].nheld:
         fr = ch0["rp"].frags()
         k = int(ch0["rp"].nheld * 2 // 3)
@@ -1000,11 +1006,11 @@ def multi_gpu(args, world, rank, local, log):
         eng_c.set_profiling(False)
         dplan.close()
         dl_ok &= bool((status == 0).all()) and bool(torch.equal(out[:nf * S], files[ch["a"] * S:ch["b"] * S]))
-    flag = torch.tensor([1 if (ok and dl_ok) else 0], dtype=torch.int32, device=dev)
+    flag = torch.tensor([1 if (ok and dl_ok) else 0], dtype=torch.int32, device=hdev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     ok_all = bool(flag.item())
     sent = {m: sum(ch["sent_" + m] for ch in sh.chunks) for m in ("ring", "star")}
-    sent_t = torch.tensor([sent["ring"], sent["star"]], dtype=torch.float64, device=dev)
+    sent_t = torch.tensor([sent["ring"], sent["star"]], dtype=torch.float64, device=hdev)
     dist.all_reduce(sent_t)
     held_bytes = sum(int(ch["lay"][N]) for ch in sh.chunks)
     res = {
@@ -1153,13 +1159,21 @@ def main():
 
     if world > 1 or args.placement_step:
         import datetime
+        if args.comm == "host":
+            # rehearsal: ranks share the GPUs present; the library's communicator goes through host
+            # shared memory (chosen by the unique id) and the harness's own collectives through gloo
+            os.environ["DFS_COMM_TRANSPORT"] = "host"
+            local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", str(_free_port()))
             os.environ.setdefault("RANK", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=600))
+        if args.comm == "host":
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=600))
         S, N, F = args.file_size, args.nfrag, args.files
         failures = []
         try:
@@ -1186,7 +1200,10 @@ def main():
                            "files_per_gpu": F, "file_bytes": S, "nfrag": N, "parallelism": f"files sharded x{world}",
                            "placement": args.placement},
                 "roofline": roofline_n(res, S, N) if ok else None,
-                "placement": res["placement"], "verified": ok})
+                "placement": res["placement"], "verified": ok,
+                **({"rehearsal": "host-staged communicator (--comm host): ranks share the GPUs present and bytes "
+                                 "cross through host memory; functional check only, the rates mean nothing"}
+                   if args.comm == "host" else {})})
         dist.destroy_process_group()
         return 0 if ok and not failures else 3
 

@@ -33,6 +33,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -49,9 +50,9 @@ static_assert(DFS_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
 struct dfs_comm {
     dfs_ctx* ctx = nullptr;
-    ncclComm_t nc = nullptr;
+    ncclComm_t nc = nullptr;       // RCCL communicator, or
+    dfs::HostComm* host = nullptr; // shared-memory mailboxes (hostcomm.cpp): exactly one of the two
     uint32_t nranks = 0, rank = 0;
-    uint64_t* d_sizes = nullptr;  // all-gather scratch (nranks * kMaxFrag words)
     uint64_t* d_gather = nullptr; // allgather_u64 scratch
     uint64_t gather_cap = 0;      // words
 };
@@ -280,22 +281,92 @@ struct RcclTransport : Transport {
     }
 };
 
+// Host-staged transport (one comm per process): the group's ops are collected
+// and run to completion at group_end, after everything queued on the ctx
+// stream before them has finished; what the caller queues next sees the data.
+struct HostTransport : Transport {
+    dfs_comm* c;
+    std::vector<HostOp> ops;
+    explicit HostTransport(dfs_comm* comm) : c(comm) {}
+    int copy(uint32_t, void* dst, const void* src, uint64_t n) override {
+        HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
+        HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, dfs::ctx_stream(c->ctx)));
+        return DFS_OK;
+    }
+    int group_start() override {
+        ops.clear();
+        return DFS_OK;
+    }
+    int send(uint32_t, const void* p, uint64_t n, int32_t peer) override {
+        ops.push_back(HostOp{true, const_cast<void*>(p), n, static_cast<uint32_t>(peer), true});
+        return DFS_OK;
+    }
+    int recv(uint32_t, void* p, uint64_t n, int32_t peer) override {
+        ops.push_back(HostOp{false, p, n, static_cast<uint32_t>(peer), true});
+        return DFS_OK;
+    }
+    int group_end() override {
+        HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
+        HIPCHK(hipStreamSynchronize(dfs::ctx_stream(c->ctx)));
+        const int rc = host_comm_exchange(c->host, ops);
+        if (rc == DFS_E_COMM) std::snprintf(g_last_comm, sizeof g_last_comm, "host transport: a peer stopped answering or sizes differ");
+        return rc;
+    }
+};
+
 int run_plans_rccl(dfs_comm* const* comms, uint32_t ncomms, const std::vector<Plan>& plans, const void* const* src,
                    void* const* dst) {
+    if (comms[0]->host) {
+        HostTransport t(comms[0]);
+        return run_plans(t, plans, src, dst);
+    }
     RcclTransport t(comms, ncomms);
     return run_plans(t, plans, src, dst);
 }
 
+// Either RCCL communicators (any number per process) or one host-staged one.
 int check_comms(dfs_comm* const* comms, uint32_t ncomms) {
     if (!comms || !ncomms) return DFS_E_ARG;
-    for (uint32_t i = 0; i < ncomms; ++i)
-        if (!comms[i] || !comms[i]->nc || comms[i]->nranks != comms[0]->nranks) return DFS_E_ARG;
+    for (uint32_t i = 0; i < ncomms; ++i) {
+        if (!comms[i] || (!comms[i]->nc && !comms[i]->host) || comms[i]->nranks != comms[0]->nranks) return DFS_E_ARG;
+        if (comms[i]->host && ncomms != 1) return DFS_E_ARG;
+    }
     return DFS_OK;
+}
+
+// All-gather of host words over a host-staged comm.
+int host_allgather(dfs_comm* c, const void* mine, uint64_t bytes, void* all) {
+    std::vector<HostOp> ops;
+    uint8_t* out = static_cast<uint8_t*>(all);
+    std::memcpy(out + bytes * c->rank, mine, bytes);
+    for (uint32_t r = 0; r < c->nranks; ++r) {
+        if (r == c->rank) continue;
+        ops.push_back(HostOp{true, const_cast<void*>(mine), bytes, r, false});
+        ops.push_back(HostOp{false, out + bytes * r, bytes, r, false});
+    }
+    return host_comm_exchange(c->host, ops);
 }
 
 dfs_ctx* comm_ctx(const dfs_comm* c) { return c->ctx; }
 
 int allreduce_u32(dfs_comm* const* comms, uint32_t ncomms, uint32_t* const* d_buf, uint32_t count) {
+    if (comms[0]->host) {  // gather every rank's words on the host, add, put the sums back
+        dfs_comm* c = comms[0];
+        hipStream_t s = dfs::ctx_stream(c->ctx);
+        HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
+        std::vector<uint32_t> mine(count), all(static_cast<size_t>(count) * c->nranks);
+        HIPCHK(hipMemcpyAsync(mine.data(), d_buf[0], 4ull * count, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (int rc = host_allgather(c, mine.data(), 4ull * count, all.data())) return rc;
+        for (uint32_t k = 0; k < count; ++k) {
+            uint32_t sum = 0;
+            for (uint32_t r = 0; r < c->nranks; ++r) sum += all[static_cast<size_t>(r) * count + k];
+            mine[k] = sum;
+        }
+        HIPCHK(hipMemcpyAsync(d_buf[0], mine.data(), 4ull * count, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return DFS_OK;
+    }
     NCCLC(ncclGroupStart());
     for (uint32_t i = 0; i < ncomms; ++i) {
         dfs_comm* c = comms[i];
@@ -314,6 +385,7 @@ int allreduce_u32(dfs_comm* const* comms, uint32_t ncomms, uint32_t* const* d_bu
 int allgather_u64(dfs_comm* const* comms, uint32_t ncomms, const uint64_t* const* mine, uint64_t count,
                   uint64_t* const* all) {
     if (!count) return DFS_OK;
+    if (comms[0]->host) return host_allgather(comms[0], mine[0], 8 * count, all[0]);
     const uint32_t W = comms[0]->nranks;
     for (uint32_t i = 0; i < ncomms; ++i) {
         dfs_comm* c = comms[i];
@@ -514,6 +586,8 @@ int dfs_place_simulate(uint32_t nranks, uint32_t nfrag, const uint64_t* table, u
 
 int dfs_comm_unique_id(uint8_t* id) {
     if (!id) return DFS_E_ARG;
+    if (const char* t = std::getenv("DFS_COMM_TRANSPORT"))
+        if (!std::strcmp(t, "host")) return dfs::host_comm_make_id(id);
     ncclUniqueId u;
     NCCLC(ncclGetUniqueId(&u));
     std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
@@ -529,6 +603,16 @@ int dfs_comm_init_rank(dfs_ctx* ctx, const uint8_t* id, uint32_t nranks, uint32_
     c->ctx = ctx;
     c->nranks = nranks;
     c->rank = rank;
+    if (dfs::host_comm_is_id(id)) {
+        const int rc = dfs::host_comm_open(id, nranks, rank, &c->host);
+        if (rc != DFS_OK) {
+            delete c;
+            if (rc == DFS_E_COMM) std::snprintf(g_last_comm, sizeof g_last_comm, "host transport: shared memory rendezvous failed");
+            return rc;
+        }
+        *out = c;
+        return DFS_OK;
+    }
     ncclUniqueId u;
     std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
     ncclResult_t r = ncclCommInitRank(&c->nc, static_cast<int>(nranks), u, static_cast<int>(rank));
@@ -574,7 +658,7 @@ int dfs_comm_destroy(dfs_comm* c) {
     (void)hipSetDevice(dfs::ctx_device(c->ctx));
     (void)hipStreamSynchronize(dfs::ctx_stream(c->ctx));
     if (c->nc) (void)ncclCommDestroy(c->nc);
-    if (c->d_sizes) (void)hipFree(c->d_sizes);
+    if (c->host) dfs::host_comm_close(c->host);
     if (c->d_gather) (void)hipFree(c->d_gather);
     delete c;
     return DFS_OK;
@@ -592,36 +676,16 @@ int dfs_place_sizes(dfs_comm* const* comms, uint32_t ncomms, const uint64_t* grp
     if (int rc = check_comms(comms, ncomms)) return rc;
     if (!grp_len || !table || !nfrag || nfrag > kMaxFrag) return DFS_E_ARG;
     const uint32_t W = comms[0]->nranks;
+    // every comm gathers the same table: keep the first
+    std::vector<std::vector<uint64_t>> all(ncomms, std::vector<uint64_t>(static_cast<size_t>(W) * nfrag));
+    std::vector<const uint64_t*> in(ncomms);
+    std::vector<uint64_t*> out(ncomms);
     for (uint32_t i = 0; i < ncomms; ++i) {
-        dfs_comm* c = comms[i];
-        HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
-        if (!c->d_sizes) HIPCHK(hipMalloc(&c->d_sizes, 8ull * (W + 1) * kMaxFrag));
-        HIPCHK(hipMemcpyAsync(c->d_sizes + static_cast<uint64_t>(W) * kMaxFrag, grp_len + static_cast<uint64_t>(i) * nfrag,
-                              8ull * nfrag, hipMemcpyHostToDevice, dfs::ctx_stream(c->ctx)));
+        in[i] = grp_len + static_cast<uint64_t>(i) * nfrag;
+        out[i] = all[i].data();
     }
-    NCCLC(ncclGroupStart());
-    for (uint32_t i = 0; i < ncomms; ++i) {
-        dfs_comm* c = comms[i];
-        if (ncomms > 1 && hipSetDevice(dfs::ctx_device(c->ctx)) != hipSuccess) {
-            (void)ncclGroupEnd();
-            return DFS_E_HIP;
-        }
-        ncclResult_t r = ncclAllGather(c->d_sizes + static_cast<uint64_t>(W) * kMaxFrag, c->d_sizes, nfrag, ncclUint64,
-                                       c->nc, dfs::ctx_stream(c->ctx));
-        if (r != ncclSuccess) {
-            (void)ncclGroupEnd();
-            return comm_fail(r, "ncclAllGather");
-        }
-    }
-    NCCLC(ncclGroupEnd());
-    // every comm gathers the same table: read it back from the first
-    dfs_comm* c = comms[0];
-    HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
-    HIPCHK(hipMemcpyAsync(table, c->d_sizes, 8ull * W * nfrag, hipMemcpyDeviceToHost, dfs::ctx_stream(c->ctx)));
-    for (uint32_t i = 0; i < ncomms; ++i) {
-        HIPCHK(hipSetDevice(dfs::ctx_device(comms[i]->ctx)));
-        HIPCHK(hipStreamSynchronize(dfs::ctx_stream(comms[i]->ctx)));
-    }
+    if (int rc = dfs::allgather_u64(comms, ncomms, in.data(), nfrag, out.data())) return rc;
+    std::memcpy(table, all[0].data(), 8ull * W * nfrag);
     return DFS_OK;
 }
 

@@ -61,4 +61,22 @@ int allgather_u64(dfs_comm* const* comms, uint32_t ncomms, const uint64_t* const
                   uint64_t* const* all);
 dfs_ctx* comm_ctx(const dfs_comm* c);
 
+// Host-staged communicator (hostcomm.cpp): the ranks are processes of one
+// host and bytes cross through shared-memory mailboxes, so several ranks can
+// share one GPU.  Chosen by the unique id (host_comm_is_id).
+struct HostComm;
+struct HostOp {
+    bool send;
+    void* p;        // device (hipMemcpy) or host memory
+    uint64_t len;
+    uint32_t peer;
+    bool device;
+};
+bool host_comm_is_id(const uint8_t* id);
+int host_comm_make_id(uint8_t* id);
+int host_comm_open(const uint8_t* id, uint32_t nranks, uint32_t rank, HostComm** out);
+void host_comm_close(HostComm* h);
+// Run this rank's sends and receives to completion (synchronous).
+int host_comm_exchange(HostComm* h, std::vector<HostOp>& ops);
+
 }  // namespace dfs

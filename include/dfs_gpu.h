@@ -489,7 +489,15 @@ int dfs_view_release(dfs_view* view);
  * several GPUs (dfs_comm_init_all, ncclCommInitAll).  The place / fetch
  * calls take an array of `ncomms` comms (1 in rank-per-process mode; all of
  * a process's comms otherwise, one source / destination pointer each) and
- * are asynchronous on each comm's ctx stream (dfs_set_stream). */
+ * are asynchronous on each comm's ctx stream (dfs_set_stream).
+ *
+ * Host-staged transport: with DFS_COMM_TRANSPORT=host in the environment
+ * dfs_comm_unique_id returns an id that makes dfs_comm_init_rank join a
+ * communicator over host shared memory instead of RCCL (every rank a process
+ * of one host, at most 16, one comm per process).  Ranks may then share a
+ * GPU, which RCCL refuses, so every multi-rank call below runs on a box with
+ * one GPU; the calls are synchronous and slow (device -> mailbox -> device in
+ * 4 MiB chunks): for tests and rehearsals. */
 #define DFS_COMM_ID_BYTES 128
 typedef struct dfs_comm dfs_comm;
 int dfs_comm_unique_id(uint8_t* id /* DFS_COMM_ID_BYTES */);

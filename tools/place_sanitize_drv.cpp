@@ -2,18 +2,24 @@
 // replica.cpp: the transfer schedules (dfs_place_plan), the runner under the
 // in-process RCCL stand-in (dfs_place_simulate) and the replica layout
 // (dfs_replica_layout), over many world sizes, fragment counts, ragged and
-// empty groups and offline masks.  Host-only: the kernel launchers and ctx
+// empty groups and offline masks; then the host-staged communicator's
+// mailboxes (hostcomm.cpp) with one thread per rank and host-memory messages
+// from one byte to several chunks.  Host-only: the kernel launchers and ctx
 // accessors are stubbed, no device is touched.  Run tools/place_sanitize.sh.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <random>
+#include <thread>
 #include <vector>
 #include "dfs_gpu.h"
 #include "dfs_internal.h"
+#include "placement_internal.h"
 namespace dfs {
 hipStream_t ctx_stream(dfs_ctx*) { return nullptr; }
 int ctx_device(dfs_ctx*) { return 0; }
+hipError_t ctx_aux_stream(dfs_ctx*, hipStream_t* aux) { *aux = nullptr; return hipSuccess; }
 uint32_t sort_sha_lanes(std::vector<ShaDesc>&) { return 0; }
 uint64_t finish_stream_jobs(std::vector<StreamJob>&, const std::vector<uint64_t>&, uint64_t) { return 0; }
 uint64_t decode_items(uint64_t, uintptr_t) { return 1; }
@@ -32,9 +38,83 @@ static int fail(const char* what, uint32_t W, uint32_t N) {
     return 1;
 }
 
+// Every rank sends two messages to every other rank per round and receives
+// theirs; message (from, to, k, round) has a length and bytes both sides can
+// compute.
+static uint64_t msg_len(uint32_t from, uint32_t to, uint32_t k, uint32_t round) {
+    static const uint64_t sizes[] = {1, 7, 4096, (4ull << 20) - 1, 4ull << 20, (4ull << 20) + 1, (9ull << 20) + 13, 70000};
+    return sizes[(from * 7 + to * 3 + k * 5 + round) % 8];
+}
+static uint8_t msg_byte(uint32_t from, uint32_t to, uint32_t k, uint32_t round, uint64_t i) {
+    return static_cast<uint8_t>(from * 31 + to * 17 + k * 5 + round * 3 + i * 7 + (i >> 11));
+}
+
+static int host_comm_cases() {
+    int cases = 0;
+    for (uint32_t W : {2u, 3u, 5u}) {
+        uint8_t id[DFS_COMM_ID_BYTES];
+        if (dfs::host_comm_make_id(id) != DFS_OK || !dfs::host_comm_is_id(id)) return -1;
+        std::atomic<int> bad{0};
+        std::vector<std::thread> th;
+        for (uint32_t me = 0; me < W; ++me)
+            th.emplace_back([&, me] {
+                dfs::HostComm* h = nullptr;
+                if (dfs::host_comm_open(id, W, me, &h) != DFS_OK) {
+                    ++bad;
+                    return;
+                }
+                for (uint32_t round = 0; round < 3; ++round) {
+                    std::vector<std::vector<uint8_t>> out, in;
+                    std::vector<dfs::HostOp> ops;
+                    for (uint32_t k = 0; k < 2; ++k)
+                        for (uint32_t r = 0; r < W; ++r) {
+                            if (r == me) continue;
+                            out.emplace_back(msg_len(me, r, k, round));
+                            for (uint64_t i = 0; i < out.back().size(); ++i) out.back()[i] = msg_byte(me, r, k, round, i);
+                            in.emplace_back(msg_len(r, me, k, round), 0xEE);
+                        }
+                    size_t q = 0;
+                    for (uint32_t k = 0; k < 2; ++k)
+                        for (uint32_t r = 0; r < W; ++r) {
+                            if (r == me) continue;
+                            // receives before sends on odd ranks: the order of posting across peers must not matter
+                            dfs::HostOp snd{true, out[q].data(), out[q].size(), r, false};
+                            dfs::HostOp rcv{false, in[q].data(), in[q].size(), r, false};
+                            if (me & 1) ops.push_back(rcv), ops.push_back(snd);
+                            else ops.push_back(snd), ops.push_back(rcv);
+                            ++q;
+                        }
+                    if (dfs::host_comm_exchange(h, ops) != DFS_OK) ++bad;
+                    q = 0;
+                    for (uint32_t k = 0; k < 2; ++k)
+                        for (uint32_t r = 0; r < W; ++r) {
+                            if (r == me) continue;
+                            for (uint64_t i = 0; i < in[q].size(); ++i)
+                                if (in[q][i] != msg_byte(r, me, k, round, i)) {
+                                    ++bad;
+                                    break;
+                                }
+                            ++q;
+                        }
+                }
+                dfs::host_comm_close(h);
+            });
+        for (auto& t : th) t.join();
+        if (bad.load()) return -1;
+        ++cases;
+    }
+    return cases;
+}
+
 int main() {
     std::mt19937_64 rng(20261113);
     int cases = 0;
+    const int hc = host_comm_cases();
+    if (hc < 0) {
+        std::printf("FAIL host-staged communicator\n");
+        return 1;
+    }
+    cases += hc;
     for (uint32_t W : {1u, 2u, 3u, 4u, 5u, 7u, 8u, 16u, 64u})
         for (uint32_t N : {1u, 2u, 3u, 5u, 8u, 10u, 64u}) {
             std::vector<uint64_t> table(static_cast<size_t>(W) * N);
