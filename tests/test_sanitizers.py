@@ -1,7 +1,9 @@
 """Host code under the sanitizers, on the CPU: the request batcher's thread
 hand-off (csrc/batcher.cpp against host stand-ins for its HIP and compute
-calls) under ThreadSanitizer and under AddressSanitizer + UBSan, and the
-placement schedules, the simulated runner and the replica layout under
+calls) and the fragment store's staging ring and I/O pool
+(csrc/fragstore.cpp, same stand-ins) under ThreadSanitizer and under
+AddressSanitizer + UBSan; the placement schedules, the simulated runner, the
+replica layout and the host-staged communicator's mailboxes under
 AddressSanitizer + UBSan.  Skipped where g++ has no sanitizer runtimes."""
 import os
 import shutil
@@ -45,3 +47,14 @@ def test_placement_and_replica_layout_under_asan(tmp_path):
     out = p.stdout + p.stderr
     assert p.returncode == 0, out[-3000:]
     assert "runtime error" not in out and "AddressSanitizer" not in out, out[-3000:]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_fragment_store_under_tsan_and_asan(tmp_path):
+    if not (_has_sanitizer("thread", tmp_path) and _has_sanitizer("address,undefined", tmp_path)):
+        pytest.skip("g++ without sanitizer runtimes")
+    p = subprocess.run(["bash", os.path.join(ROOT, "tools", "fragstore_sanitize.sh")], capture_output=True, text=True,
+                       env=dict(os.environ, OUT=str(tmp_path)), timeout=800)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out[-3000:]
+    assert out.count("fragstore_sanitize_drv: 0 failed checks") == 2 and "Sanitizer" not in out, out[-3000:]
