@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <thread>
@@ -42,7 +43,15 @@ namespace {
 
 constexpr char kMagic[16] = "DFS-HOST-COMM-1";  // 15 chars + NUL
 constexpr uint64_t kSlot = 4ull << 20;
-constexpr double kTimeoutS = 120.0;
+// Seconds without progress after which a rendezvous or an exchange gives up
+// (a peer died or never came): 120, or DFS_HOST_COMM_TIMEOUT_S.
+double timeout_s() {
+    if (const char* e = std::getenv("DFS_HOST_COMM_TIMEOUT_S")) {
+        const double v = std::atof(e);
+        if (v > 0) return v;
+    }
+    return 120.0;
+}
 
 struct Header {
     std::atomic<uint32_t> attached;
@@ -112,9 +121,10 @@ int host_comm_open(const uint8_t* id, uint32_t nranks, uint32_t rank, HostComm**
     // a fresh object is zero-filled: counters start at 0.  Wait for every rank.
     h->hdr()->attached.fetch_add(1, std::memory_order_acq_rel);
     const auto t0 = Clock::now();
+    const double limit = timeout_s();
     bool ok = true;
     while (h->hdr()->attached.load(std::memory_order_acquire) < nranks) {
-        if (since(t0) > kTimeoutS) {
+        if (since(t0) > limit) {
             ok = false;
             break;
         }
@@ -148,6 +158,7 @@ int host_comm_exchange(HostComm* h, std::vector<HostOp>& ops) {
         left += o.len != 0;
     }
     auto t_last = Clock::now();
+    const double limit = timeout_s();
     while (left) {
         bool moved = false;
         // first unfinished op per (peer, direction)
@@ -192,7 +203,7 @@ int host_comm_exchange(HostComm* h, std::vector<HostOp>& ops) {
         if (moved) {
             t_last = Clock::now();
         } else {
-            if (since(t_last) > kTimeoutS) return DFS_E_COMM;  // a peer is gone
+            if (since(t_last) > limit) return DFS_E_COMM;  // a peer is gone
             std::this_thread::sleep_for(std::chrono::microseconds(20));
         }
     }

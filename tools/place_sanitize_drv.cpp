@@ -106,9 +106,64 @@ static int host_comm_cases() {
     return cases;
 }
 
+// Failure handling of the host-staged communicator, with a 1 s limit: a rank
+// that never joins, a peer that posts nothing, two sides that disagree on a
+// size.  Every call must come back with DFS_E_COMM, none may hang.
+static int host_comm_failures() {
+    setenv("DFS_HOST_COMM_TIMEOUT_S", "1", 1);
+    uint8_t id[DFS_COMM_ID_BYTES];
+    // 1. two of three ranks show up: the rendezvous gives up
+    if (dfs::host_comm_make_id(id) != DFS_OK) return -1;
+    {
+        std::atomic<int> comm_err{0};
+        std::vector<std::thread> th;
+        for (uint32_t me = 0; me < 2; ++me)
+            th.emplace_back([&, me] {
+                dfs::HostComm* h = nullptr;
+                if (dfs::host_comm_open(id, 3, me, &h) == DFS_E_COMM && !h) ++comm_err;
+            });
+        for (auto& t : th) t.join();
+        if (comm_err.load() != 2) return -1;
+    }
+    // 2. rank 1 posts nothing: rank 0's receive gives up; 3. sizes differ: the receiver refuses
+    for (int scenario = 0; scenario < 2; ++scenario) {
+        if (dfs::host_comm_make_id(id) != DFS_OK) return -1;
+        std::atomic<int> good{0};
+        std::vector<std::thread> th;
+        for (uint32_t me = 0; me < 2; ++me)
+            th.emplace_back([&, me] {
+                dfs::HostComm* h = nullptr;
+                if (dfs::host_comm_open(id, 2, me, &h) != DFS_OK) return;
+                std::vector<uint8_t> buf(1000, 7);
+                std::vector<dfs::HostOp> ops;
+                if (scenario == 0) {
+                    if (me == 0) ops.push_back(dfs::HostOp{false, buf.data(), 100, 1, false});
+                    const int rc = dfs::host_comm_exchange(h, ops);
+                    if (rc == (me == 0 ? DFS_E_COMM : DFS_OK)) ++good;
+                } else {
+                    if (me == 0) ops.push_back(dfs::HostOp{true, buf.data(), 200, 1, false});
+                    else ops.push_back(dfs::HostOp{false, buf.data(), 100, 0, false});
+                    const int rc = dfs::host_comm_exchange(h, ops);
+                    if (rc == (me == 0 ? DFS_OK : DFS_E_COMM)) ++good;  // the sender's chunk fitted its mailbox
+                }
+                dfs::host_comm_close(h);
+            });
+        for (auto& t : th) t.join();
+        if (good.load() != 2) return -1;
+    }
+    unsetenv("DFS_HOST_COMM_TIMEOUT_S");
+    return 3;
+}
+
 int main() {
     std::mt19937_64 rng(20261113);
     int cases = 0;
+    const int hf = host_comm_failures();
+    if (hf < 0) {
+        std::printf("FAIL host-staged communicator failure handling\n");
+        return 1;
+    }
+    cases += hf;
     const int hc = host_comm_cases();
     if (hc < 0) {
         std::printf("FAIL host-staged communicator\n");
