@@ -58,3 +58,51 @@ def test_static_entry_matches_batch_entry_two_calls():
         assert rc == L.DFS_E_TOOBIG
         assert b"at most 65,536" in dfs_amd.lib().dfs_strerror(rc)
         assert sha256_static_device(eng, 0, 0, 0, 0) == L.DFS_OK
+
+
+def test_static_entry_in_a_captured_graph():
+    """The allocation-free entry under stream capture: one call recorded into a
+    HIP graph (torch.cuda.graph on the engine's stream), then replayed four
+    times over new input bytes, with eager work (the input refill, the
+    reference digests through dfs_sha256_batch on another ctx) and device
+    synchronisations between the replays.  Every replay's digests are checked
+    against the eager result: the kernels' queue words and descriptors are
+    re-initialised by the entry's own prep kernel inside the graph."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(7)
+    n = 30000  # the persistent kernel
+    lens = rng.integers(0, 1500, n).astype(np.uint64)
+    offs = np.cumsum(lens + 3) - (lens + 3)
+    spans = np.stack([offs, lens], axis=1).astype(np.uint64)
+    total = int(offs[-1] + lens[-1]) + 64
+    gen = torch.Generator(device=dev).manual_seed(99)
+    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=gen)
+    d_spans = torch.from_numpy(spans.view(np.int64).copy()).to(dev)
+    d_dig = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+    d_st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    with dfs_amd.FragmentEngine(0) as eng, dfs_amd.FragmentEngine(0) as ref:
+        s = torch.cuda.Stream(dev)
+        eng.set_stream(s.cuda_stream)
+        args = (data.data_ptr(), d_spans.data_ptr(), n, d_dig.data_ptr(), d_st.data_ptr())
+        assert sha256_static_device(eng, *args) == L.DFS_OK  # eager once: everything lazy is loaded
+        torch.cuda.synchronize(dev)
+        print("static entry: capturing one call into a graph", flush=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            rc = sha256_static_device(eng, *args)
+        assert rc == L.DFS_OK
+        for rep in range(4):
+            data.copy_(torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=gen))  # eager work
+            d_dig.zero_()
+            d_st.fill_(7)
+            torch.cuda.synchronize(dev)
+            want = sha256_device(ref, data.data_ptr(), spans)  # eager, another ctx; synchronises
+            print(f"static entry: graph replay {rep + 1}", flush=True)
+            g.replay()
+            torch.cuda.synchronize(dev)
+            got = d_dig.view(n, 32).cpu().numpy()
+            assert (d_st.cpu().numpy() == 0).all(), rep
+            bad = np.nonzero((got != want).any(axis=1))[0]
+            assert bad.size == 0, f"replay {rep + 1}: {bad.size} digests differ, first at message {bad[:5]}"
+        eng.set_stream(0)
