@@ -18,7 +18,9 @@ Workloads (BASELINE.json configs):
          all-to-all; ring: primary scatter + replica step g -> g-1).
 `python bench.py --gpus N` launches its own N ranks (torch.distributed.run)
 when WORLD_SIZE is not set; rank 0 prints ONE JSON line and the exit code is
-non-zero if any leg failed or mismatched.
+non-zero if any leg failed or mismatched.  `--gpus N --comm host --files F`
+rehearses the N > 1 step with N rank processes on fewer GPUs (the library's
+host-staged communicator instead of RCCL): a functional check, the line says so.
 
 Extra objects on the line:
   roofline      dominant kernel (multi-message SHA-256) vs the int32-VALU peak,
