@@ -1,6 +1,7 @@
 #!/bin/bash
-# Encode with aligned chunk stores for packed destinations: the Base64 and
-# wire-codec tests, then the packed / aligned layouts and the wire leg again.
+# After a change to the encode kernel: the Base64, upload and wire-codec
+# tests, then the packed / aligned layouts and the wire leg
+# (scripts/gpu_r03_align_probe.sh).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
