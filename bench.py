@@ -126,6 +126,9 @@ def parse(argv=None):
     ap.add_argument("--store-files", type=int, default=2048, help="files in the on-disk fragment store leg")
     ap.add_argument("--no-store", action="store_true", help="skip the on-disk fragment store leg")
     ap.add_argument("--no-batcher", action="store_true", help="skip the concurrent-clients (batcher) leg")
+    ap.add_argument("--no-rehearsal", action="store_true",
+                    help="skip the 8-rank rehearsal of the N > 1 step on this GPU (host-staged communicator; part of "
+                         "the scaling-reference leg, so --no-scaling-ref skips it too)")
     ap.add_argument("--no-scaling-ref", action="store_true",
                     help="N=1: skip the leg that runs the N>1 step (upload + placement + holders' verify on BASELINE "
                          "configs[2]'s shard) on this one GPU, the equal-workload reference for the N>1 lines")
@@ -1437,6 +1440,36 @@ def main():
             result["n_gt_1_step_on_one_gpu"] = {"error": repr(e)[:300]}
             failures.append("n_gt_1_step_on_one_gpu")
         args.no_batcher = False  # the upload plan is closed
+        # The same step with 8 rank processes on this one GPU, through the
+        # library's host-staged communicator (small shards; functional only:
+        # BASELINE configs[2] and configs[4] end to end but for the RCCL wire).
+        # Reported, never fatal to the line: it is evidence, not the metric.
+        if not args.no_rehearsal:
+            try:
+                cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "8", "--comm", "host", "--files", "512",
+                       "--steps", "1", "--warmup", "1", "--placement", args.placement]
+                p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+                line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+                if p.returncode != 0 or not line:
+                    raise LegError(f"rehearsal child rc {p.returncode}: {p.stderr[-300:]}")
+                r = json.loads(line[-1])
+                pl = r["placement"]
+                result["multi_rank_rehearsal"] = {
+                    "ranks": 8, "gpus": 1, "files_per_rank": 512, "file_bytes": r["config"]["file_bytes"],
+                    "nfrag": r["config"]["nfrag"], "verified": r["verified"],
+                    "all_replicas_good": pl["receive_verify"]["all_replicas_good"],
+                    "corrupt_probe_caught": pl["receive_verify"]["corrupt_probe_caught"],
+                    "ring_equals_star": pl["ring_equals_star"],
+                    "degraded_read_ok": pl["degraded"]["ok"], "offline_rank": pl["degraded"]["offline_gpu"],
+                    "note": "bench.py --gpus 8 --comm host: the N>1 step (sharded upload, star and ring placement, digest "
+                            "exchange, every holder's decode + SHA-256 + compare, a corrupted replica that must be "
+                            "caught, the degraded read with the last rank offline) with 8 rank processes sharing this "
+                            "GPU over the library's host-staged communicator instead of RCCL; functional check, no rates"}
+                log(f"8-rank rehearsal on one GPU: verified={r['verified']}")
+            except Exception as e:
+                import traceback
+                traceback.print_exc()
+                result["multi_rank_rehearsal"] = {"error": repr(e)[:300]}
     if failures:
         result["failed_legs"] = failures
     emit(result)
