@@ -132,6 +132,9 @@ SIGNATURES = {
     "dfs_submit_upload_view": (_int, [_vp, _vp, _u64, _vp, _vp, ctypes.POINTER(_vp), _vp, ctypes.POINTER(_vp)]),
     "dfs_submit_download_view": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
     "dfs_view_release": (_int, [_vp]),
+    "dfs_store_hash_response_cap": (_u64, []),
+    "dfs_store_hash_responses_build": (_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, _vp, _u64, _vp]),
+    "dfs_store_hash_responses_check": (_int, [_vp, _vp, ctypes.c_uint32, _vp, _vp, _vp]),
     "dfs_comm_unique_id": (_int, [_vp]),
     "dfs_comm_init_rank": (_int, [_vp, _vp, _u32, _u32, ctypes.POINTER(_vp)]),
     "dfs_comm_init_all": (_int, [_vp, _u32, _vp]),

@@ -170,28 +170,64 @@ struct Cluster {
     }
     Node& node(int id) { return nodes[id - 1]; }
 
-    // handleInternalStoreFragments (SN:265-293) on node `id`; returns the
-    // {index -> hash} the node replies with (buildHashResponse, SN:644-655).
-    std::map<int, std::string> storeFragments(int id, const std::string& body) {
+    // What a peer answers: the reply text on the wire (buildHashResponse,
+    // SN:644-655) and, for the log lines, the {index -> hash} behind it.
+    struct StoreReply {
+        std::string json;
+        std::map<int, std::string> hashes;
+    };
+
+    // buildHashResponse through the ABI (dfs_store_hash_responses_build) for one body's two entries.
+    static std::string hashResponse(const std::string& fileId, const std::vector<std::pair<int, std::string>>& put) {
+        if (fileId.size() != 64 || put.size() != 2) {
+            // not a sendFragmentsToNode body (two entries, a SHA-256 fileId): the reference's builder as text;
+            // indices below 16 iterate in ascending order in its HashMap
+            std::map<int, std::string> m;
+            for (auto& kv : put) m[kv.first] = kv.second;
+            std::string out = "{\"fileId\":\"" + fileId + "\",\"received\":[";
+            size_t k = 0;
+            for (auto& kv : m)
+                out += "{\"index\":\"" + std::to_string(kv.first) + "\",\"hash\":\"" + kv.second + "\"}" +
+                       (++k < m.size() ? "," : "");
+            return out + "]}";
+        }
+        const uint32_t idx[2] = {static_cast<uint32_t>(put[0].first), static_cast<uint32_t>(put[1].first)};
+        dfs::Bytes dig = dfs::unhex(put[0].second), d2 = dfs::unhex(put[1].second);
+        dig.insert(dig.end(), d2.begin(), d2.end());
+        std::string out(dfs_store_hash_response_cap(), '\0');
+        uint64_t off[2] = {0, 0};
+        if (dfs_store_hash_responses_build(fileId.data(), idx, dig.data(), nullptr, 1, &out[0], out.size(), off) != DFS_OK)
+            throw std::runtime_error("dfs_store_hash_responses_build");
+        out.resize(off[1]);
+        return out;
+    }
+
+    // handleInternalStoreFragments (SN:265-293) on node `id`.
+    StoreReply storeFragments(int id, const std::string& body) {
         Node& n = node(id);
         if (!n.up) throw std::runtime_error("Connection refused");
-        std::map<int, std::string> resp;
+        StoreReply r;
+        std::vector<std::pair<int, std::string>> put;  // response.put(index, hash) in body order, SN:287
         std::string fileId;
         std::vector<std::pair<int, std::pair<dfs::Bytes, std::string>>> dev;
         if (eng.receiveStoreBody(body, fileId, dev)) {  // device parse + decode + hash
             for (auto& kv : dev) {
                 n.saveFragment(fileId, kv.first, kv.second.first);  // Files.write(<i>.frag), SN:284-285
-                resp[kv.first] = kv.second.second;
+                r.hashes[kv.first] = kv.second.second;
+                put.emplace_back(kv.first, kv.second.second);
             }
-            return resp;
+        } else {
+            auto parsed = parseJson(body);  // any other body form: the reference's parser
+            fileId = parsed.first;
+            auto got = eng.storeFragments(parsed.second);
+            for (auto& kv : got) {
+                n.saveFragment(parsed.first, kv.first, kv.second.first);  // Files.write(<i>.frag), SN:284-285
+                r.hashes[kv.first] = kv.second.second;
+                put.emplace_back(kv.first, kv.second.second);
+            }
         }
-        auto parsed = parseJson(body);  // any other body form: the reference's parser
-        auto got = eng.storeFragments(parsed.second);
-        for (auto& kv : got) {
-            n.saveFragment(parsed.first, kv.first, kv.second.first);  // Files.write(<i>.frag), SN:284-285
-            resp[kv.first] = kv.second.second;
-        }
-        return resp;
+        r.json = hashResponse(fileId, put);
+        return r;
     }
 
     // handleUpload on node u (SN:118-189).
@@ -221,13 +257,22 @@ struct Cluster {
                     const std::string& body = bodies[j];
                     if (body != dfs::buildFragmentsJson(fileId, {&up.second[f1], &up.second[f2]}))
                         throw std::logic_error("device body differs from buildFragmentsJson");
-                    auto remote = storeFragments(k + 1, body);
-                    ok = true;
-                    for (int fi : {f1, f2}) {  // SN:250-257
-                        if (remote[fi] != up.second[fi].hash) {
+                    const StoreReply remote = storeFragments(k + 1, body);
+                    // parseResponseHashes + the comparison of SN:248-257 through the ABI, on the reply text
+                    const uint32_t idx[2] = {static_cast<uint32_t>(f1), static_cast<uint32_t>(f2)};
+                    dfs::Bytes want = dfs::unhex(up.second[f1].hash), w2 = dfs::unhex(up.second[f2].hash);
+                    want.insert(want.end(), w2.begin(), w2.end());
+                    const dfs_span sp{0, remote.json.size()};
+                    int32_t st = 0;
+                    (void)dfs_store_hash_responses_check(remote.json.data(), &sp, 1, idx, want.data(), &st);
+                    ok = st == DFS_OK;
+                    for (int fi : {f1, f2}) {  // the reference's log line for a mismatch, SN:253-254
+                        auto it = remote.hashes.find(fi);
+                        const std::string rh = it == remote.hashes.end() ? "null" : it->second;
+                        if (!ok && rh != up.second[fi].hash) {
                             out.printf("[%d] Hash mismatch on fragment %d (local=%s, remote=%s)\n", u, fi,
-                                        up.second[fi].hash.c_str(), remote[fi].c_str());
-                            ok = false;
+                                        up.second[fi].hash.c_str(), rh.c_str());
+                            break;  // return false at the first one, SN:255
                         }
                     }
                 } catch (const std::exception&) {

@@ -318,6 +318,27 @@ int dfs_store_bodies_receive(dfs_ctx* ctx, const char* bodies, const dfs_span* b
                              uint64_t* frag_len, uint8_t* digests, char* file_ids, int32_t* status,
                              uint32_t flags);
 
+/* The reply half of the exchange, on the host (a reply is ~200 bytes).
+ * Receiver: buildHashResponse (SN:644-655) over the HashMap filled by
+ * response.put(index, hash) (SN:277-288), for the n bodies of one
+ * dfs_store_bodies_receive call: file_ids (64 chars per body), frag_index
+ * (2 per body), digests (2 x 32 raw bytes per body) and status are that
+ * call's outputs; a body whose status is not 0 gets no reply (its handler
+ * threw, SN:280-282: the sender sees a dropped connection).  Replies are
+ * written back to back into out (NULL: lengths only), out_off[n + 1]; a
+ * reply is at most dfs_store_hash_response_cap() bytes.
+ * Sender: parseResponseHashes (SN:657-701) and the comparison of SN:248-257
+ * for n replies (spans into `responses`; len 0 = no reply): frag_index and
+ * expected (2 x 32 raw bytes per body) are what the sender put into body i.
+ * status[i] = 0, DFS_E_FRAG_MISMATCH ("Hash mismatch on fragment", or no
+ * entry for a fragment) or DFS_E_WIRE (where the Java parser throws); each
+ * makes that attempt fail (SN:212-221).  Returns 0 or the first failure. */
+uint64_t dfs_store_hash_response_cap(void);
+int dfs_store_hash_responses_build(const char* file_ids, const uint32_t* frag_index, const uint8_t* digests,
+                                   const int32_t* status, uint32_t n, char* out, uint64_t out_cap, uint64_t* out_off);
+int dfs_store_hash_responses_check(const char* responses, const dfs_span* spans, uint32_t n,
+                                   const uint32_t* frag_index, const uint8_t* expected, int32_t* status);
+
 /* ---- on-disk fragment store (SN:147-149, 163-166, 273-285, 463-469) ------ */
 /* A node's fragments live at
  *   <node_root>/<fileId hex>/fragments/<index>.frag
