@@ -58,3 +58,14 @@ def test_fragment_store_under_tsan_and_asan(tmp_path):
     out = p.stdout + p.stderr
     assert p.returncode == 0, out[-3000:]
     assert out.count("fragstore_sanitize_drv: 0 failed checks") == 2 and "Sanitizer" not in out, out[-3000:]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_reply_parser_fuzz_under_asan(tmp_path):
+    if not _has_sanitizer("address,undefined", tmp_path):
+        pytest.skip("g++ without sanitizer runtimes")
+    p = subprocess.run(["bash", os.path.join(ROOT, "tools", "wire_sanitize.sh")], capture_output=True, text=True,
+                       env=dict(os.environ, OUT=str(tmp_path)), timeout=600)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0 and "wire_sanitize_drv: 200000 replies" in out, out[-3000:]
+    assert "runtime error" not in out and "AddressSanitizer" not in out, out[-3000:]
