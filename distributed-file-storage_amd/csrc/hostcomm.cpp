@@ -55,7 +55,7 @@ double timeout_s() {
 
 struct Header {
     std::atomic<uint32_t> attached;
-    uint32_t nranks;
+    std::atomic<uint32_t> nranks;  // set by the first rank to attach; the others must agree
     uint8_t pad[56];
 };
 
@@ -107,7 +107,10 @@ int host_comm_open(const uint8_t* id, uint32_t nranks, uint32_t rank, HostComm**
     for (int i = 0; i < 12; ++i) p += std::snprintf(p, 3, "%02x", id[sizeof kMagic + i]);
     h->bytes = sizeof(Header) + sizeof(Box) * static_cast<size_t>(nranks) * nranks;
     const int fd = shm_open(h->name, O_CREAT | O_RDWR, 0600);
-    if (fd < 0 || ftruncate(fd, static_cast<off_t>(h->bytes)) != 0) {
+    struct stat sb;
+    // grow only: a rank that disagrees on the world size must not shrink what others have mapped
+    if (fd < 0 || fstat(fd, &sb) != 0 ||
+        (static_cast<size_t>(sb.st_size) < h->bytes && ftruncate(fd, static_cast<off_t>(h->bytes)) != 0)) {
         if (fd >= 0) close(fd);
         delete h;
         return DFS_E_COMM;
@@ -119,11 +122,12 @@ int host_comm_open(const uint8_t* id, uint32_t nranks, uint32_t rank, HostComm**
         return DFS_E_COMM;
     }
     // a fresh object is zero-filled: counters start at 0.  Wait for every rank.
+    uint32_t seen = 0;
+    bool ok = h->hdr()->nranks.compare_exchange_strong(seen, nranks) || seen == nranks;  // same world size everywhere
     h->hdr()->attached.fetch_add(1, std::memory_order_acq_rel);
     const auto t0 = Clock::now();
     const double limit = timeout_s();
-    bool ok = true;
-    while (h->hdr()->attached.load(std::memory_order_acquire) < nranks) {
+    while (ok && h->hdr()->attached.load(std::memory_order_acquire) < nranks) {
         if (since(t0) > limit) {
             ok = false;
             break;
