@@ -952,6 +952,37 @@ def multi_gpu(args, world, rank, local, log):
         sh.upload(c, flags)
         sha_ms.append(eng.timings()["sha"])
     eng.set_profiling(False)
+    # Every file this rank uploaded against the oracle (outside the timing):
+    # fileIds, fragment digests and, through a device SHA-256 of each
+    # fragment's Base64, the Base64 (as the N = 1 line does); mismatches are
+    # summed over the ranks.
+    oracle_check, oracle_ok = None, True
+    if args.verify and args.verify_all:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # checker only
+        from dfs_amd.engine import sha256_device
+        _, threads = host_cpu_info()
+        threads = max(1, threads // world)  # the ranks share the host's cores
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        efd, efrd, eb64 = O.synth_digests(rank * F, F, S, N, threads)
+        t_cpu = time.perf_counter() - t0
+        bad_fd = int((sh.fd.view(F, 32).cpu().numpy() != efd).any(axis=1).sum())
+        bad_frd = int((sh.frd.view(F, N, 32).cpu().numpy() != efrd).any(axis=2).sum())
+        bad_b64 = 0
+        for ch in sh.chunks:
+            nf = ch["b"] - ch["a"]
+            got = sha256_device(eng, ch["b64"].data_ptr(), ch["plan"].b64_spans([S] * nf)).reshape(nf, N, 32)
+            bad_b64 += int((got != eb64[ch["a"]:ch["b"]]).any(axis=2).sum())
+        bad = torch.tensor([bad_fd, bad_frd, bad_b64], dtype=torch.int64, device=hdev)
+        dist.all_reduce(bad)
+        oracle_check = {"files_per_rank": F, "ranks": world, "file_digests_checked": F * world,
+                        "fragment_digests_checked": F * N * world, "base64_fragments_checked": F * N * world,
+                        "mismatches": int(bad.sum().item()), "oracle_seconds": round(t_cpu, 2), "oracle_threads": threads,
+                        "how": "every rank checks its own shard: oracle C path (libcrypto SHA-256, scalar Base64) over "
+                               "each synthetic file; the device Base64 through a per-fragment SHA-256 on the device"}
+        oracle_ok = oracle_check["mismatches"] == 0
+        log(f"oracle check of every rank's {F} files: {oracle_check['mismatches']} mismatches ({t_cpu:.1f} s, {threads} threads per rank)")
     t_place = {}
     for mode in ("star", "ring"):
         step(mode, compute=False, verify=False)
@@ -971,7 +1002,7 @@ def multi_gpu(args, world, rank, local, log):
     dig_ring = held_digests()
     step("star", compute=False, verify=False)
     torch.cuda.synchronize(dev)
-    ok = dig_ring == held_digests() and verify_ok
+    ok = dig_ring == held_digests() and verify_ok and oracle_ok
     # Degraded read (BASELINE configs[4]): the last GPU offline; every other
     # rank fetches its groups back from the live holders (SN:422-446), then
     # Base64-decodes them into place with per-fragment and fileId verify.
@@ -1052,7 +1083,7 @@ def multi_gpu(args, world, rank, local, log):
                     "dfs_place_star); download = Base64 decode into place + fragment and fileId SHA-256 verify of "
                     "the fetched groups (dfs_download_plan_run: tables prebuilt, download_plan_ms once per shape), wall "
                     "clock and HIP-event device time"},
-        "sha_ms_per_launch": float(np.mean(sha_ms)), "files_per_launch": F / C, "ok": ok_all}
+        "sha_ms_per_launch": float(np.mean(sha_ms)), "files_per_launch": F / C, "ok": ok_all, "verify": oracle_check}
     for ch in sh.chunks:
         ch["plan"].close()
         ch["rp"].close()
@@ -1205,7 +1236,7 @@ def main():
                            "files_per_gpu": F, "file_bytes": S, "nfrag": N, "parallelism": f"files sharded x{world}",
                            "placement": args.placement},
                 "roofline": roofline_n(res, S, N) if ok else None,
-                "placement": res["placement"], "verified": ok,
+                "placement": res["placement"], "verified": ok, "verify": res.get("verify"),
                 **({"rehearsal": "host-staged communicator (--comm host): ranks share the GPUs present and bytes "
                                  "cross through host memory; functional check only, the rates mean nothing"}
                    if args.comm == "host" else {})})
