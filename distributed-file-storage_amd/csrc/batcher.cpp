@@ -246,6 +246,7 @@ struct dfs_batcher {
     bool stop = false;
     std::vector<Worker*> workers;
     dfs_batcher_stats_t st{};
+    bool dl_in_kernel = true;  // direct downloads: Base64 in by one copy kernel (else one DMA per request); DFS_BATCH_DL_IN=dma
 };
 
 namespace {
@@ -455,7 +456,7 @@ int run_downloads(dfs_batcher* B, Worker& w, std::vector<Req*>& batch, BatchSync
             d += sp.len;
         }
     }
-    if (int e = move_in(w, cp, true)) return e;
+    if (int e = move_in(w, cp, B->dl_in_kernel)) return e;
     std::vector<int32_t> st(n);
     rc = dfs_download_batch(w.ctx, w.d_in.as<char>(), spans.data(), n, N, file_len.data(), have_f ? ef.data() : nullptr,
                             have_i ? ei.data() : nullptr, w.d_out.as<uint8_t>(), file_off.data(), st.data(),
@@ -667,6 +668,7 @@ int dfs_batcher_create(int device, uint32_t nfrag, const dfs_batcher_opts* opts,
     B->device = device;
     B->nfrag = nfrag;
     B->o = dfs_batcher_opts{200, 1024, 1ull << 30, 2};
+    if (const char* e = std::getenv("DFS_BATCH_DL_IN")) B->dl_in_kernel = std::strcmp(e, "dma") != 0;
     if (opts) {
         if (opts->max_wait_us) B->o.max_wait_us = opts->max_wait_us;
         if (opts->max_files) B->o.max_files = opts->max_files;
