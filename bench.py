@@ -570,13 +570,14 @@ def batcher_leg(args, log):
     """Thread-per-connection clients (SN:28-31), one 1 MiB file per request,
     through the library's batcher (dfs_submit_upload / dfs_submit_download,
     host buffers: PCIe in and out) at each concurrency in --clients, closed
-    loop for --client-seconds, in three buffer modes: "staged" (pageable
+    loop for --client-seconds, in four buffer modes: "staged" (pageable
     handler buffers: each handler copies its bytes into and out of the
     worker's pinned staging), "pinned" (handler buffers from
     dfs_host_alloc: the worker's DMA reads / writes them, no host copies) and
     "view" (pinned inputs; the answer stays in the batch's pinned result
     buffer and the handler gets a pointer: dfs_submit_*_view, one DMA out per
-    batch instead of one per request).
+    batch instead of one per request) and "staged_view" (pageable inputs
+    copied into the staging, the answer as a view: one DMA each way).
     The clients are native threads (tools/batcher_load, a child process); the
     fileIds it reports are checked here.  Beside it the CPU proxy at the same
     concurrency (min(C, cores) threads, one file per thread), upload and
@@ -591,7 +592,7 @@ def batcher_leg(args, log):
     rows, ok, cpu_one = [], True, None
     for C in [int(x) for x in args.clients.split(",") if x]:
         row = {"clients": C}
-        for pinned in (0, 1, 2):
+        for pinned in (0, 1, 2, 3):
             for kind in ("upload", "download"):
                 p = subprocess.run([tool, str(C), str(args.client_seconds), kind, str(S), str(N), "2000", "3",
                                     str(pinned)], capture_output=True, text=True, timeout=300)
@@ -600,12 +601,12 @@ def batcher_leg(args, log):
                                    f"{p.stdout[-300:]}")
                 r = json.loads(p.stdout.strip().splitlines()[-1])
                 ok &= r["ok"] and [r["file0_id"], r["file1_id"]] == want
-                key = kind + ("", "_pinned", "_view")[pinned]
+                key = kind + ("", "_pinned", "_view", "_staged_view")[pinned]
                 row[key] = {k: r[k] for k in ("requests", "gbps", "p50_ms", "p99_ms")}
                 st = r["stats"]
                 row[key]["batches"] = st["batches"]
                 row[key]["direct"] = st["direct"]
-                if pinned == 2:
+                if pinned >= 2:
                     row[key]["views"] = st["views"]
                 row[key]["mean_batch"] = round(st["requests"] / max(st["batches"], 1), 1)
                 row[key]["device_ms_per_batch"] = round(st["device_s"] / max(st["batches"], 1) * 1e3, 2)
@@ -640,9 +641,9 @@ def batcher_leg(args, log):
     info, _ = host_cpu_info()
     one_up = next((r["cpu_upload_gbps"] for r in rows if r["cpu_threads"] == 1 and r["cpu_upload_gbps"]), None)
     one_dn = next((r["cpu_download_gbps"] for r in rows if r["cpu_threads"] == 1 and r["cpu_download_gbps"]), None)
-    best_up = max((max(r[k]["gbps"] for k in ("upload", "upload_pinned", "upload_view")) for r in rows), default=None)
-    best_dn = max((max(r[k]["gbps"] for k in ("download", "download_pinned", "download_view")) for r in rows),
-                  default=None)
+    modes = ("", "_pinned", "_view", "_staged_view")
+    best_up = max((max(r["upload" + m]["gbps"] for m in modes) for r in rows), default=None)
+    best_dn = max((max(r["download" + m]["gbps"] for m in modes) for r in rows), default=None)
     proj = None
     if one_up and one_dn:
         proj = {"single_thread_upload_gbps": one_up, "single_thread_download_gbps": one_dn, "hosts": []}
@@ -664,13 +665,16 @@ def batcher_leg(args, log):
                                   "upload_pinned": cross("upload_pinned", "cpu_upload_gbps"),
                                   "download_pinned": cross("download_pinned", "cpu_download_gbps"),
                                   "upload_view": cross("upload_view", "cpu_upload_gbps"),
-                                  "download_view": cross("download_view", "cpu_download_gbps")},
+                                  "download_view": cross("download_view", "cpu_download_gbps"),
+                                  "upload_staged_view": cross("upload_staged_view", "cpu_upload_gbps"),
+                                  "download_staged_view": cross("download_staged_view", "cpu_download_gbps")},
             "ok": ok, "cpu_cores": cores, "full_host_cpu_projection": proj,
             "note": "native client threads (tools/batcher_load, 3 workers, 2 ms window), host buffers: each request "
                     "crosses PCIe in and out; staged = pageable handler buffers copied by the handler into / out of "
                     "pinned staging, pinned = dfs_host_alloc buffers moved by DMA directly (direct = such requests), view = pinned "
                     "inputs, the answer left in the batch's pinned result buffer and handed out as a pointer "
-                    "(dfs_submit_*_view: one DMA out per batch); "
+                    "(dfs_submit_*_view: one DMA out per batch), staged_view = pageable inputs copied by the handler into "
+                    "the staging (one DMA in) with the answer as a view (one DMA out, no copy back); "
                     "latency = one handler's blocking call; cpu = the oracle's C proxy with min(C, cores) threads "
                     "(OpenSSL SHA-256 + scalar Base64, upload and download sequences); cpu_latency_est = one file's "
                     "single-thread time x ceil(C / threads); crossover = fewest clients where the GPU path beats the "

@@ -11,7 +11,8 @@
 // pinned = 1: every client's buffers come from dfs_host_alloc (direct
 // requests: DMA straight from / into them, no staging copies); pinned = 2:
 // pinned inputs and the outputs as views (dfs_submit_*_view: the answer stays
-// in the batch's result buffer, one DMA per batch, released after the check).
+// in the batch's result buffer, one DMA per batch, released after the check);
+// pinned = 3: pageable inputs (staged by the handler) with view outputs.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -134,7 +135,7 @@ int main(int argc, char** argv) {
     if (argc > 6) o.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
     if (argc > 7) o.depth = static_cast<uint32_t>(std::atoi(argv[7]));
     const int pin_mode = argc > 8 ? std::atoi(argv[8]) : 0;
-    const bool pinned = pin_mode != 0, views = pin_mode == 2;
+    const bool pinned = pin_mode == 1 || pin_mode == 2, views = pin_mode >= 2;  // 3: pageable inputs, view outputs
     // A client buffer: pageable (std::vector) or a slice of one dfs_host_alloc
     // pool (a server would pin its connection buffers once, not per request;
     // one pool instead of 3 x C pinned allocations also keeps the setup of
