@@ -1077,6 +1077,9 @@ def multi_gpu(args, world, rank, local, log):
             "ring_xgmi_gbps_per_gpu": round(sent_t[0].item() / world / t_place["ring"] / 1e9, 2),
             "bytes_sent_per_gpu": {"star": int(sent_t[1].item() / world), "ring": int(sent_t[0].item() / world)},
             "held_bytes_per_gpu": held_bytes, "ring_equals_star": ok,
+            "transfers_issued": dict(comm.counters(), loopback=os.environ.get("DFS_COMM_LOOPBACK") == "1",
+                                     note="this rank's sends / receives / local copies over the whole run; with "
+                                          "DFS_COMM_LOOPBACK=1 the local copies travel as ncclSend / ncclRecv to itself"),
             "degraded": {"offline_gpu": offline[0] if offline else None, "fetch_ms": round(fetch_ms, 3),
                          "download_ms": round(dl_ms, 3), "download_device_ms": round(dl_dev_ms, 3),
                          "download_plan_ms": round(dl_plan_ms, 2),

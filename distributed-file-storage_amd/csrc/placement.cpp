@@ -55,7 +55,20 @@ struct dfs_comm {
     uint32_t nranks = 0, rank = 0;
     uint64_t* d_gather = nullptr; // allgather_u64 scratch
     uint64_t gather_cap = 0;      // words
+    // DFS_COMM_LOOPBACK=1 when the comm was made: a rank's local copies go
+    // through ncclSend / ncclRecv to itself inside the phase's group instead of
+    // hipMemcpyAsync, so a one-rank run drives the same RCCL calls, group
+    // bracketing and stream ordering as a many-rank one.  For tests.
+    bool loopback = false;
+    uint64_t issued[3] = {0, 0, 0};  // sends, receives, local copies (dfs_comm_counters)
 };
+
+namespace {
+bool env_loopback() {
+    const char* e = std::getenv("DFS_COMM_LOOPBACK");
+    return e && e[0] == '1';
+}
+}  // namespace
 
 using dfs::holder_a;
 using dfs::holder_b;
@@ -213,14 +226,14 @@ int run_plans(Transport& t, const std::vector<Plan>& plans, const void* const* s
         // local copies first (same stream as the group: ordered before it)
         for (uint32_t i = 0; i < n; ++i)
             for (const dfs_xfer& x : plans[i].ops) {
-                if (x.phase != ph || x.kind != DFS_XFER_COPY) continue;
+                if (x.phase != ph || x.kind != DFS_XFER_COPY || t.self_peer(i) >= 0) continue;
                 const char* from = x.from_dst ? static_cast<const char*>(dst[i]) : static_cast<const char*>(src[i]);
                 if (int rc = t.copy(i, static_cast<char*>(dst[i]) + x.dst_off, from + x.src_off, x.len)) return rc;
             }
         bool any = false;
         for (uint32_t i = 0; i < n && !any; ++i)
             for (const dfs_xfer& x : plans[i].ops)
-                if (x.phase == ph && x.kind != DFS_XFER_COPY) {
+                if (x.phase == ph && (x.kind != DFS_XFER_COPY || t.self_peer(i) >= 0)) {
                     any = true;
                     break;
                 }
@@ -228,9 +241,13 @@ int run_plans(Transport& t, const std::vector<Plan>& plans, const void* const* s
         if (int rc = t.group_start()) return rc;
         for (uint32_t i = 0; i < n; ++i)
             for (const dfs_xfer& x : plans[i].ops) {
-                if (x.phase != ph || x.kind == DFS_XFER_COPY) continue;
+                if (x.phase != ph || (x.kind == DFS_XFER_COPY && t.self_peer(i) < 0)) continue;
                 int rc;
-                if (x.kind == DFS_XFER_SEND) {
+                if (x.kind == DFS_XFER_COPY) {
+                    const char* from = x.from_dst ? static_cast<const char*>(dst[i]) : static_cast<const char*>(src[i]);
+                    rc = t.send(i, from + x.src_off, x.len, t.self_peer(i));
+                    if (!rc) rc = t.recv(i, static_cast<char*>(dst[i]) + x.dst_off, x.len, t.self_peer(i));
+                } else if (x.kind == DFS_XFER_SEND) {
                     const char* from = x.from_dst ? static_cast<const char*>(dst[i]) : static_cast<const char*>(src[i]);
                     rc = t.send(i, from + x.src_off, x.len, x.peer);
                 } else {
@@ -259,26 +276,54 @@ struct RcclTransport : Transport {
     int copy(uint32_t i, void* dst, const void* src, uint64_t n) override {
         if (int rc = use(i)) return rc;
         HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, dfs::ctx_stream(comms[i]->ctx)));
+        ++comms[i]->issued[2];
         return DFS_OK;
     }
     int group_start() override {
         NCCLC(ncclGroupStart());
         return DFS_OK;
     }
+    // One transfer goes out as pieces of at most piece_bytes(), the same split
+    // on the sending and the receiving side (both know the length), so the
+    // pieces pair in posting order like whole transfers do.  RCCL 2.26 was seen
+    // to leave parts of a 1.4 GB send-to-self unwritten (358 MB and below were
+    // complete); bounded pieces keep every count inside what was checked on
+    // hardware, for peers as well.
+    static uint64_t piece_bytes() {
+        static const uint64_t v = [] {
+            const char* e = std::getenv("DFS_COMM_PIECE_MB");
+            const long mb = e ? std::atol(e) : 0;
+            return (mb > 0 ? static_cast<uint64_t>(mb) : 256ull) << 20;
+        }();
+        return v;
+    }
     int send(uint32_t i, const void* p, uint64_t n, int32_t peer) override {
         if (int rc = use(i)) return rc;
-        const ncclResult_t r = ncclSend(p, n, ncclUint8, peer, comms[i]->nc, dfs::ctx_stream(comms[i]->ctx));
-        return r == ncclSuccess ? DFS_OK : comm_fail(r, "ncclSend");
+        const char* b = static_cast<const char*>(p);
+        for (uint64_t o = 0; o < n; o += piece_bytes()) {  // plans hold no empty transfers
+            const uint64_t len = n - o < piece_bytes() ? n - o : piece_bytes();
+            const ncclResult_t r = ncclSend(b + o, len, ncclUint8, peer, comms[i]->nc, dfs::ctx_stream(comms[i]->ctx));
+            ++comms[i]->issued[0];
+            if (r != ncclSuccess) return comm_fail(r, "ncclSend");
+        }
+        return DFS_OK;
     }
     int recv(uint32_t i, void* p, uint64_t n, int32_t peer) override {
         if (int rc = use(i)) return rc;
-        const ncclResult_t r = ncclRecv(p, n, ncclUint8, peer, comms[i]->nc, dfs::ctx_stream(comms[i]->ctx));
-        return r == ncclSuccess ? DFS_OK : comm_fail(r, "ncclRecv");
+        char* b = static_cast<char*>(p);
+        for (uint64_t o = 0; o < n; o += piece_bytes()) {  // plans hold no empty transfers
+            const uint64_t len = n - o < piece_bytes() ? n - o : piece_bytes();
+            const ncclResult_t r = ncclRecv(b + o, len, ncclUint8, peer, comms[i]->nc, dfs::ctx_stream(comms[i]->ctx));
+            ++comms[i]->issued[1];
+            if (r != ncclSuccess) return comm_fail(r, "ncclRecv");
+        }
+        return DFS_OK;
     }
     int group_end() override {
         NCCLC(ncclGroupEnd());
         return DFS_OK;
     }
+    int32_t self_peer(uint32_t i) const override { return comms[i]->loopback ? static_cast<int32_t>(comms[i]->rank) : -1; }
 };
 
 // Host-staged transport (one comm per process): the group's ops are collected
@@ -291,6 +336,7 @@ struct HostTransport : Transport {
     int copy(uint32_t, void* dst, const void* src, uint64_t n) override {
         HIPCHK(hipSetDevice(dfs::ctx_device(c->ctx)));
         HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, dfs::ctx_stream(c->ctx)));
+        ++c->issued[2];
         return DFS_OK;
     }
     int group_start() override {
@@ -299,10 +345,12 @@ struct HostTransport : Transport {
     }
     int send(uint32_t, const void* p, uint64_t n, int32_t peer) override {
         ops.push_back(HostOp{true, const_cast<void*>(p), n, static_cast<uint32_t>(peer), true});
+        ++c->issued[0];
         return DFS_OK;
     }
     int recv(uint32_t, void* p, uint64_t n, int32_t peer) override {
         ops.push_back(HostOp{false, p, n, static_cast<uint32_t>(peer), true});
+        ++c->issued[1];
         return DFS_OK;
     }
     int group_end() override {
@@ -448,9 +496,11 @@ struct SimTransport : dfs::Transport {
     };
     uint32_t W;
     bool open = false;
+    bool loop = env_loopback();  // copies as self send / receive pairs, as on an RCCL comm made with the same setting
     std::map<std::pair<uint32_t, uint32_t>, std::vector<Op>> sends, recvs;  // key = (from, to)
     std::string err;
     explicit SimTransport(uint32_t w) : W(w) {}
+    int32_t self_peer(uint32_t i) const override { return loop ? static_cast<int32_t>(i) : -1; }
     int fail(const std::string& m) {
         err = m;
         std::snprintf(g_last_comm, sizeof g_last_comm, "simulated exchange: %s", m.c_str());
@@ -469,7 +519,7 @@ struct SimTransport : dfs::Transport {
         return DFS_OK;
     }
     int send(uint32_t i, const void* p, uint64_t n, int32_t peer) override {
-        if (!open || peer < 0 || static_cast<uint32_t>(peer) >= W || static_cast<uint32_t>(peer) == i)
+        if (!open || peer < 0 || static_cast<uint32_t>(peer) >= W || (static_cast<uint32_t>(peer) == i && !loop))
             return fail("bad send");
         Op o;
         o.src = static_cast<const char*>(p);
@@ -478,7 +528,7 @@ struct SimTransport : dfs::Transport {
         return DFS_OK;
     }
     int recv(uint32_t i, void* p, uint64_t n, int32_t peer) override {
-        if (!open || peer < 0 || static_cast<uint32_t>(peer) >= W || static_cast<uint32_t>(peer) == i)
+        if (!open || peer < 0 || static_cast<uint32_t>(peer) >= W || (static_cast<uint32_t>(peer) == i && !loop))
             return fail("bad recv");
         Op o;
         o.dst = static_cast<char*>(p);
@@ -620,6 +670,7 @@ int dfs_comm_init_rank(dfs_ctx* ctx, const uint8_t* id, uint32_t nranks, uint32_
         delete c;
         return comm_fail(r, "ncclCommInitRank");
     }
+    c->loopback = env_loopback();
     *out = c;
     return DFS_OK;
 }
@@ -648,6 +699,7 @@ int dfs_comm_init_all(dfs_ctx* const* ctxs, uint32_t n, dfs_comm** out) {
         c->nc = nc[i];
         c->nranks = n;
         c->rank = i;
+        c->loopback = env_loopback();
         out[i] = c;
     }
     return DFS_OK;
@@ -668,6 +720,12 @@ int dfs_comm_info(const dfs_comm* c, uint32_t* nranks, uint32_t* rank) {
     if (!c) return DFS_E_ARG;
     if (nranks) *nranks = c->nranks;
     if (rank) *rank = c->rank;
+    return DFS_OK;
+}
+
+int dfs_comm_counters(const dfs_comm* c, uint64_t* counters) {
+    if (!c || !counters) return DFS_E_ARG;
+    std::memcpy(counters, c->issued, sizeof c->issued);
     return DFS_OK;
 }
 

@@ -43,10 +43,15 @@ struct Transport {
     virtual int send(uint32_t i, const void* p, uint64_t n, int32_t peer) = 0;
     virtual int recv(uint32_t i, void* p, uint64_t n, int32_t peer) = 0;
     virtual int group_end() = 0;
+    // Rank of endpoint i if its local copies are to travel as a send to itself
+    // paired with a receive from itself inside the phase's group, else -1.
+    virtual int32_t self_peer(uint32_t) const { return -1; }
 };
 
 // Issue every plan's ops phase by phase: local copies, then one group with
-// the phase's sends and receives of every endpoint, in plan order.
+// the phase's sends and receives of every endpoint, in plan order.  On an
+// endpoint with a self_peer the copies are posted in the group as well, as
+// send + receive pairs to itself.
 int run_plans(Transport& t, const std::vector<Plan>& plans, const void* const* src, void* const* dst);
 
 // RCCL transport over `comms` (every op on its comm's ctx stream).

@@ -140,6 +140,7 @@ SIGNATURES = {
     "dfs_comm_init_all": (_int, [_vp, _u32, _vp]),
     "dfs_comm_destroy": (_int, [_vp]),
     "dfs_comm_info": (_int, [_vp, _vp, _vp]),
+    "dfs_comm_counters": (_int, [_vp, _vp]),
     "dfs_comm_last_error": (ctypes.c_char_p, []),
     "dfs_place_sizes": (_int, [_vp, _u32, _vp, _u32, _vp]),
     "dfs_place_plan": (_int, [_u32, _u32, _u32, _vp, _u32, _u64, _vp, _vp, _vp, _vp]),

@@ -171,6 +171,12 @@ class Comm:
     def _arr(self):
         return (ctypes.c_void_p * 1)(self._c.value)
 
+    def counters(self) -> dict:
+        """Transfers issued on this comm so far: sends, receives, local copies."""
+        c = np.zeros(3, dtype=np.uint64)
+        _comm_error(lib().dfs_comm_counters(self._c, c.ctypes.data), "dfs_comm_counters")
+        return {"sends": int(c[0]), "recvs": int(c[1]), "copies": int(c[2])}
+
     def sizes(self, grp_len: Sequence[int]) -> np.ndarray:
         """(world, nfrag) table of every rank's group bytes (synchronous)."""
         g = np.ascontiguousarray(grp_len, dtype=np.uint64)

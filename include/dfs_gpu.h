@@ -518,7 +518,13 @@ int dfs_view_release(dfs_view* view);
  * of one host, at most 16, one comm per process).  Ranks may then share a
  * GPU, which RCCL refuses, so every multi-rank call below runs on a box with
  * one GPU; the calls are synchronous and slow (device -> mailbox -> device in
- * 4 MiB chunks): for tests and rehearsals. */
+ * 4 MiB chunks): for tests and rehearsals.
+ *
+ * Loopback: a comm made while DFS_COMM_LOOPBACK=1 is in the environment posts
+ * a rank's local copies as ncclSend to itself paired with ncclRecv from itself
+ * inside the phase's group instead of hipMemcpyAsync, so a one-rank run on one
+ * GPU drives the same RCCL calls, group bracketing and stream ordering as a
+ * many-rank one.  For tests; results are identical. */
 #define DFS_COMM_ID_BYTES 128
 typedef struct dfs_comm dfs_comm;
 int dfs_comm_unique_id(uint8_t* id /* DFS_COMM_ID_BYTES */);
@@ -526,6 +532,9 @@ int dfs_comm_init_rank(dfs_ctx* ctx, const uint8_t* id, uint32_t nranks, uint32_
 int dfs_comm_init_all(dfs_ctx* const* ctxs, uint32_t n, dfs_comm** comms);
 int dfs_comm_destroy(dfs_comm* comm);
 int dfs_comm_info(const dfs_comm* comm, uint32_t* nranks, uint32_t* rank);
+/* Transfers the place / fetch / verify calls have issued on this comm since
+ * it was made: counters[0] sends, [1] receives, [2] local copies. */
+int dfs_comm_counters(const dfs_comm* comm, uint64_t* counters /* 3 */);
 /* Text of the last RCCL failure on this thread (DFS_E_COMM). */
 const char* dfs_comm_last_error(void);
 

@@ -20,9 +20,23 @@ from dfs_amd import placement as P
 from test_placement_plan import _groups
 
 
+@pytest.fixture(params=[False, True], ids=["copies", "loopback"])
+def loopback(request, monkeypatch):
+    """With DFS_COMM_LOOPBACK=1 the runner posts a rank's local copies as a
+    send to itself paired with a receive from itself inside the phase's group
+    (what a one-rank RCCL run uses to drive ncclSend / ncclRecv); the simulated
+    transport then also checks that no such pair reads bytes the same group
+    writes."""
+    if request.param:
+        monkeypatch.setenv("DFS_COMM_LOOPBACK", "1")
+    else:
+        monkeypatch.delenv("DFS_COMM_LOOPBACK", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("world,nfrag", [(2, 5), (2, 8), (4, 4), (4, 8), (8, 8), (8, 5), (3, 8), (5, 5), (1, 5)])
 @pytest.mark.parametrize("mode", ["ring", "star"])
-def test_native_runner_places_like_the_reference(world, nfrag, mode):
+def test_native_runner_places_like_the_reference(world, nfrag, mode, loopback):
     rng = np.random.default_rng(world * 131 + nfrag)
     table, src = _groups(world, nfrag, rng)
     blobs = [b"".join(g) for g in src]
@@ -37,7 +51,7 @@ def test_native_runner_places_like_the_reference(world, nfrag, mode):
 
 
 @pytest.mark.parametrize("world,nfrag", [(2, 5), (4, 4), (4, 8), (8, 8), (8, 5), (5, 5)])
-def test_native_runner_degraded_fetch(world, nfrag):
+def test_native_runner_degraded_fetch(world, nfrag, loopback):
     rng = np.random.default_rng(world + 11 * nfrag)
     table, src = _groups(world, nfrag, rng)
     held, _ = P.simulate_native(world, nfrag, table, "star", [b"".join(g) for g in src])
