@@ -23,11 +23,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 
-@pytest.mark.parametrize("placement,extra", [("star", []), ("ring", ["--file-size", "1000003", "--nfrag", "5"])])
-def test_placement_step_through_rccl_send_recv(placement, extra):
+# piece_mb: the runner splits every transfer into pieces of at most that many MiB (256 by default; RCCL was seen
+# to lose bytes of a 1.4 GB send-to-self), the same split on both sides; 1 MiB makes these small groups many pieces
+@pytest.mark.parametrize("placement,extra,piece_mb", [("star", [], 0), ("ring", ["--file-size", "1000003", "--nfrag", "5"], 1)])
+def test_placement_step_through_rccl_send_recv(placement, extra, piece_mb):
     files = 256
-    print(f"RCCL loopback: 1 rank x {files} files, {placement} {extra}", flush=True)
+    print(f"RCCL loopback: 1 rank x {files} files, {placement} {extra} piece_mb={piece_mb}", flush=True)
     env = dict(os.environ, DFS_COMM_LOOPBACK="1")
+    if piece_mb:
+        env["DFS_COMM_PIECE_MB"] = str(piece_mb)
     p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--placement-step", "--files", str(files),
                         "--steps", "1", "--warmup", "1", "--placement", placement, "--no-cpu-baseline"] + extra,
                        capture_output=True, text=True, timeout=240, env=env)
