@@ -168,6 +168,21 @@ class Comm:
         _comm_error(lib().dfs_comm_init_rank(engine.ctx, idb, world, rank, ctypes.byref(self._c)),
                     "dfs_comm_init_rank")
 
+    @classmethod
+    def init_all(cls, engines) -> "List[Comm]":
+        """dfs_comm_init_all: one process driving one communicator per engine
+        (one engine per GPU; ncclCommInitAll), rank i on engines[i]."""
+        n = len(engines)
+        ctxs = (ctypes.c_void_p * n)(*[e.ctx for e in engines])
+        out = (ctypes.c_void_p * n)()
+        _comm_error(lib().dfs_comm_init_all(ctxs, n, out), "dfs_comm_init_all")
+        comms = []
+        for i, e in enumerate(engines):
+            c = cls.__new__(cls)
+            c.engine, c.world, c.rank, c._c = e, n, i, ctypes.c_void_p(out[i])
+            comms.append(c)
+        return comms
+
     def _arr(self):
         return (ctypes.c_void_p * 1)(self._c.value)
 

@@ -506,6 +506,32 @@ def test_rccl_placement_single_rank(engine):
         plan.close()
 
 
+def test_comm_init_all_one_gpu(engine):
+    """dfs_comm_init_all (one process, one communicator per GPU through
+    ncclCommInitAll) with the one GPU present: the comm reports world 1 /
+    rank 0, gathers sizes and places like one made from a unique id."""
+    import ctypes
+    import torch
+    from dfs_amd import _lib as L
+    from dfs_amd import placement as P
+    (comm,) = P.Comm.init_all([engine])
+    try:
+        nr, rk = ctypes.c_uint32(9), ctypes.c_uint32(9)
+        assert L.lib().dfs_comm_info(comm._c, ctypes.byref(nr), ctypes.byref(rk)) == 0 and (nr.value, rk.value) == (1, 0)
+        sizes = [1000, 0, 77, 4096, 5]
+        table = comm.sizes(sizes)
+        assert table.tolist() == [sizes]
+        src = torch.randint(0, 256, (sum(sizes),), dtype=torch.uint8, device="cuda")
+        lay = P.held_layout(1, 0, len(sizes), table)
+        held = torch.zeros(int(lay[len(sizes)]), dtype=torch.uint8, device="cuda")
+        comm.place("ring", table, src.data_ptr(), held.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(held, src)
+        assert comm.counters() == {"sends": 0, "recvs": 0, "copies": 4}  # the empty group is skipped
+    finally:
+        comm.close()
+
+
 def test_sha256_update_streaming(engine, golden):
     """Chunked SHA-256 with carried state == one-shot digest (skew config's
     streaming path), for several chunkings, message lengths and alignments."""
