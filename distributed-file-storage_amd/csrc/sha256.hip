@@ -126,6 +126,12 @@ __device__ __forceinline__ void to_be(uint32_t (&r)[16], uint32_t x, uint32_t se
     r[15] = __builtin_amdgcn_perm(x, r[15], sel);
 }
 
+// Block k of the message at p.  The offset is formed in 64 bits: 16 * k dwords
+// no longer fit 32 bits from a 16 GiB message on (k >= 2^28).
+__device__ __forceinline__ const uint32_t* blk(const uint32_t* __restrict__ p, uint32_t k) {
+    return p + (static_cast<uint64_t>(k) << 4);
+}
+
 // Per-lane message geometry.
 struct Msg {
     const uint32_t* p;  // dword-aligned pointer at or below the first byte
@@ -155,7 +161,7 @@ __device__ __forceinline__ Msg msg_setup(const uint8_t* __restrict__ base, const
 __device__ __forceinline__ void tail_block(const Msg& m, uint32_t tb, uint32_t (&W)[16]) {
     const uint32_t r = static_cast<uint32_t>(m.len) & 63u;
     const uint32_t lim = m.len ? m.sh + r : 0u;  // tail word i holds message bytes iff 4i < lim
-    const uint32_t* __restrict__ q = m.p + 16u * m.nfull;
+    const uint32_t* __restrict__ q = blk(m.p, m.nfull);
     uint32_t T[17];
 #pragma unroll
     for (int i = 0; i < 17; ++i) {
@@ -202,20 +208,20 @@ __device__ __forceinline__ void init_state(uint32_t (&st)[8]) {
 __device__ __forceinline__ void plain_range(uint32_t (&st)[8], const Msg& m, uint32_t kb, uint32_t ke) {
     uint32_t A[16], B[16], C[16], D[16], xa, xb, xc, xd;
     const uint32_t last = ke - 1u;
-    load_block(m.p + 16u * kb, m.sh, A, xa);
-    load_block(m.p + 16u * min(kb + 1u, last), m.sh, B, xb);
+    load_block(blk(m.p, kb), m.sh, A, xa);
+    load_block(blk(m.p, min(kb + 1u, last)), m.sh, B, xb);
     uint32_t k = kb;
     for (;;) {
-        load_block(m.p + 16u * min(k + 2u, last), m.sh, C, xc);
-        load_block(m.p + 16u * min(k + 3u, last), m.sh, D, xd);
+        load_block(blk(m.p, min(k + 2u, last)), m.sh, C, xc);
+        load_block(blk(m.p, min(k + 3u, last)), m.sh, D, xd);
         to_be(A, xa, m.sel);
         compress(st, A);
         if (++k >= ke) break;
         to_be(B, xb, m.sel);
         compress(st, B);
         if (++k >= ke) break;
-        load_block(m.p + 16u * min(k + 2u, last), m.sh, A, xa);
-        load_block(m.p + 16u * min(k + 3u, last), m.sh, B, xb);
+        load_block(blk(m.p, min(k + 2u, last)), m.sh, A, xa);
+        load_block(blk(m.p, min(k + 3u, last)), m.sh, B, xb);
         to_be(C, xc, m.sel);
         compress(st, C);
         if (++k >= ke) break;
@@ -234,14 +240,14 @@ __device__ __forceinline__ void twin_range(uint32_t (&st)[8], uint32_t (&s2)[8],
                                            uint32_t ke) {
     uint32_t A[16], B[16], xa, xb;
     const uint32_t last = ke - 1u;
-    load_block(m.p + 16u * kb, m.sh, A, xa);
+    load_block(blk(m.p, kb), m.sh, A, xa);
     uint32_t k = kb;
     for (;;) {
-        load_block(m.p + 16u * min(k + 1u, last), m.sh, B, xb);
+        load_block(blk(m.p, min(k + 1u, last)), m.sh, B, xb);
         to_be(A, xa, m.sel);
         compress2(st, s2, A);
         if (++k >= ke) break;
-        load_block(m.p + 16u * min(k + 1u, last), m.sh, A, xa);
+        load_block(blk(m.p, min(k + 1u, last)), m.sh, A, xa);
         to_be(B, xb, m.sel);
         compress2(st, s2, B);
         if (++k >= ke) break;
@@ -582,7 +588,7 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                     uint32_t k = 0;
 #define DFS_SHA_STEP(PH)                                                          \
     {                                                                             \
-        load_block(bp + 16u * min(k + 1u, last), m.sh, N, xn);                    \
+        load_block(blk(bp, min(k + 1u, last)), m.sh, N, xn);                    \
         to_be(C, xc, m.sel);                                                      \
         if (enc && k < m.nfull) {                                                 \
             enc_block<PH>(pair, C, prev, bdst, P);                                \
@@ -808,11 +814,11 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
         uint32_t R[16], Q[16], xr, xq;
         load_block(bp, sh, R, xr);
         if (kmax) helper_block(m, nb, 0, R, xr, kw[0] + lane);
-        load_block(bp + 16u * min(1u, last), sh, R, xr);
+        load_block(blk(bp, min(1u, last)), sh, R, xr);
         __syncthreads();
         for (uint32_t k = 0; k < kmax; ++k) {
             if (k + 1 < kmax) {
-                load_block(bp + 16u * min(k + 2u, last), sh, Q, xq);
+                load_block(blk(bp, min(k + 2u, last)), sh, Q, xq);
                 helper_block(m, nb, k + 1, R, xr, kw[(k + 1) & 1u] + lane);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) R[i] = Q[i];

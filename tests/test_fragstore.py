@@ -162,6 +162,7 @@ def test_device_store_round_trip(tmp_path, monkeypatch, engine, slot_mb):
     assert (st == 0).all()
     assert O.py_tree(store.root) == _oracle_tree(tmp_path, files, 5, 4)
     d_back = torch.zeros_like(d_buf)
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     st, ln = store.read(dig, d_back.data_ptr(), refs, device=True)
     assert (st == 0).all() and list(ln) == [len(b) for b in blobs]
     assert d_back.cpu().numpy().tobytes() == buf.tobytes()
@@ -195,6 +196,7 @@ def test_device_config1_download_from_disk(tmp_path, engine, example_bytes):
         assert (stores[k].write(dig, d_files.data_ptr(), make_refs(off, ln, fi, ix), device=True) == 0).all()
     # download plan (SN:421-451): local first, then holders in order, node `down` offline
     d_frag = torch.zeros(sum(S) + 64, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     addr = np.zeros(len(files) * N, dtype=np.uint64)
     flen = np.zeros(len(files) * N, dtype=np.uint64)
     per_node = {}
@@ -210,6 +212,7 @@ def test_device_config1_download_from_disk(tmp_path, engine, example_bytes):
         st, got = stores[src].read(dig, d_frag.data_ptr(), make_refs(off, ln, fi, ix), device=True)
         assert (st == 0).all() and list(got) == list(ln)
     d_out = torch.zeros(sum(S) + 64, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     st, fdig = reassemble_device(engine, addr, flen, len(files), N, d_out.data_ptr(), base, expected=dig)
     assert (st == 0).all() and (fdig == dig).all()
     assert d_out[:sum(S)].cpu().numpy().tobytes() == b"".join(files)

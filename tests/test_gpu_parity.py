@@ -351,6 +351,7 @@ def test_device_plan_and_synth_vs_oracle(engine):
     fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
     frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
     b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     engine.set_stream(torch.cuda.current_stream().cuda_stream)
     try:
         for flags in (0, dfs_amd.DFS_SERIAL):
@@ -389,6 +390,7 @@ def test_align128_plan(monkeypatch, mode):
         fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
         frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
         b64 = torch.full((plan.b64_total,), 0xAA, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
         torch.cuda.synchronize()
         bsp = plan.b64_spans(lens)
@@ -408,6 +410,7 @@ def test_align128_plan(monkeypatch, mode):
         gaps = np.frombuffer(blob, dtype=np.uint8)[~covered]
         assert (gaps == 0xAA).all()
         out = torch.zeros(int(offs_f[-1]) + 1, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         st = download_device(eng, b64.data_ptr(), bsp, nfiles, nfrag, np.array(lens, dtype=np.uint64),
                              frd.data_ptr(), fd.data_ptr(), out.data_ptr(), offs_f[:-1].copy())
         torch.cuda.synchronize()
@@ -433,6 +436,7 @@ def test_frag_major_plan_and_device_download(engine):
     fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
     frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
     b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
     torch.cuda.synchronize()
     offs = plan.b64_offsets()
@@ -446,6 +450,7 @@ def test_frag_major_plan_and_device_download(engine):
             k = f * nfrag + i
             assert blob[int(msp[k, 0]):int(msp[k, 0] + msp[k, 1])] == O.c_b64_encode(d[o:o + ln])
     out = torch.zeros(nfiles * S, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     st = download_device(engine, b64.data_ptr(), msp, nfiles, nfrag, np.full(nfiles, S, np.uint64),
                          frd.data_ptr(), fd.data_ptr(), out.data_ptr(),
                          np.arange(nfiles, dtype=np.uint64) * np.uint64(S))
@@ -472,6 +477,7 @@ def test_rccl_placement_single_rank(engine):
     fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
     frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
     b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
     torch.cuda.synchronize()
     offs = plan.b64_offsets()
@@ -484,6 +490,7 @@ def test_rccl_placement_single_rank(engine):
         held = {}
         for mode in ("ring", "star"):
             h = torch.zeros(int(lay[nfrag]), dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
             comm.place(mode, table, b64.data_ptr(), h.data_ptr())
             torch.cuda.synchronize()
             held[mode] = h
@@ -494,6 +501,7 @@ def test_rccl_placement_single_rank(engine):
         torch.cuda.synchronize()
         assert (st == 0).all() and torch.equal(back, b64)
         out = torch.zeros(nfiles * S, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         status = download_device(engine, back.data_ptr(), plan.b64_spans([S] * nfiles), nfiles, nfrag,
                                  np.full(nfiles, S, np.uint64), frd.data_ptr(), fd.data_ptr(), out.data_ptr(),
                                  np.arange(nfiles, dtype=np.uint64) * np.uint64(S))
@@ -522,8 +530,10 @@ def test_comm_init_all_one_gpu(engine):
         table = comm.sizes(sizes)
         assert table.tolist() == [sizes]
         src = torch.randint(0, 256, (sum(sizes),), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         lay = P.held_layout(1, 0, len(sizes), table)
         held = torch.zeros(int(lay[len(sizes)]), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         comm.place("ring", table, src.data_ptr(), held.data_ptr())
         torch.cuda.synchronize()
         assert torch.equal(held, src)
@@ -891,6 +901,7 @@ def test_device_download_verdicts(engine, mode, monkeypatch):
         fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
         frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
         b64 = torch.zeros(plan.b64_total, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
         torch.cuda.synchronize()
         msp = P.frag_major_spans([S] * nfiles, nfrag).copy()
@@ -905,6 +916,7 @@ def test_device_download_verdicts(engine, mode, monkeypatch):
         msp[9 * nfrag + 4, 1] = np.uint64(dfs_amd.DFS_SPAN_MISSING)
         want[9] = dfs_amd.DFS_E_MISSING
         out = torch.zeros(nfiles * S, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         st = download_device(engine, b64.data_ptr(), msp, nfiles, nfrag, np.full(nfiles, S, np.uint64),
                              frd.data_ptr(), fd.data_ptr(), out.data_ptr(),
                              np.arange(nfiles, dtype=np.uint64) * np.uint64(S))
@@ -920,10 +932,12 @@ def test_device_download_verdicts(engine, mode, monkeypatch):
         dplan = dfs_amd.DownloadPlan(engine, msp, nfiles, nfrag, flen, foff)
         for rep in range(3):
             out.zero_()
+            torch.cuda.synchronize()
             st = dplan.run(b64.data_ptr(), frd.data_ptr(), fd.data_ptr(), out.data_ptr())
             assert st.tolist() == want.tolist(), rep
             assert torch.equal(out.view(nfiles, S)[torch.as_tensor(good)], f0[torch.as_tensor(good)]), rep
         b64[int(msp[k, 0]) + 5] = ord("A")  # a valid char, but not the encoder's: the fragment digest differs
+        torch.cuda.synchronize()
         st = dplan.run(b64.data_ptr(), frd.data_ptr(), fd.data_ptr(), out.data_ptr())
         want2 = want.copy()
         want2[7] = dfs_amd.DFS_E_FRAG_MISMATCH

@@ -29,11 +29,13 @@ def _run(engine, lens, nfrag, align128, seed):
     spans = np.stack([offs, np.array(lens, dtype=np.uint64)], axis=1)
     total = int(sum(lens))
     files = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     dfs_amd.synth_fill(engine, files.data_ptr(), spans, seed, O.SYNTH_SEED)
     plan = dfs_amd.UploadPlan(engine, spans, nfrag, frag_major=True, align128=align128)
     fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device=dev)
     frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device=dev)
     b64 = torch.zeros(max(plan.b64_total, 1), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), 0)
     torch.cuda.synchronize()
     comm = P.Comm(engine, P.unique_id(), 1, 0)
@@ -66,10 +68,12 @@ def test_replica_verify_single_rank(engine, align128, shape, slices, monkeypatch
         assert rp.table.tolist() == comm.sizes([grp[f + 1] - grp[f] for f in range(nfrag)]).tolist()
         assert rp.nheld == len(lens) * nfrag and rp.held_bytes == grp[-1]
         held = torch.zeros(max(rp.held_bytes, 1), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         comm.place("star", rp.table, c["b64"].data_ptr(), held.data_ptr())
         raw = torch.zeros(rp.raw_bytes + 16, dtype=torch.uint8, device=dev)
         verdict = torch.full((rp.nheld,), 99, dtype=torch.int32, device=dev)
         failed = torch.full((1,), 99, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
         print(f"replica verify {shape} align128={align128} slices={slices}: {rp.nheld} held fragments", flush=True)
         rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
         torch.cuda.synchronize()
@@ -88,12 +92,14 @@ def test_replica_verify_single_rank(engine, align128, shape, slices, monkeypatch
         p1 = int(frags[k1]["b64_off"]) + 5
         old = int(held[p1])
         held[p1] = ord("B") if old == ord("A") else ord("A")
+        torch.cuda.synchronize()
         rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
         torch.cuda.synchronize()
         v = verdict.cpu().numpy()
         assert np.nonzero(v)[0].tolist() == [k1] and v[k1] == L.DFS_E_FRAG_MISMATCH and int(failed[0]) == 1
         # and one byte outside the alphabet in another fragment: the decoder's IllegalArgumentException (SN:281)
         held[int(frags[k2]["b64_off"]) + 2] = ord("!")
+        torch.cuda.synchronize()
         rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
         torch.cuda.synchronize()
         v = verdict.cpu().numpy()
@@ -104,6 +110,7 @@ def test_replica_verify_single_rank(engine, align128, shape, slices, monkeypatch
         held[int(frags[k2]["b64_off"]) + 2] = ord("A")
         frd2 = c["frd"].clone()
         frd2[32 * 7 + 3] ^= 1  # file 1, fragment 2 of [file][fragment] (nfrag >= 5)
+        torch.cuda.synchronize()
         rp.verify(frd2.data_ptr(), held.data_ptr(), raw.data_ptr(), 0, failed.data_ptr())
         torch.cuda.synchronize()
         assert int(failed[0]) >= 1

@@ -164,6 +164,7 @@ def test_hybrid_upload_plan_device(hybrid_engine, align128, frag_major):
             fd = torch.zeros(nfiles * 32, dtype=torch.uint8, device="cuda")
             frd = torch.zeros(nfiles * nfrag * 32, dtype=torch.uint8, device="cuda")
             b64 = torch.zeros(plan.b64_total + 64, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
             plan.run(files.data_ptr(), fd.data_ptr(), frd.data_ptr(), b64.data_ptr(), flags)
             torch.cuda.synchronize()
             if not flags:

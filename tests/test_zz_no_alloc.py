@@ -22,11 +22,13 @@ def _case(eng, torch, dev, rng, n, max_len):
     total = int(offs[-1] + lens[-1]) + 64
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev,
                          generator=torch.Generator(device=dev).manual_seed(int(rng.integers(1 << 30))))
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     spans = np.stack([offs, lens], axis=1).astype(np.uint64)
     want = sha256_device(eng, data.data_ptr(), spans)                     # dfs_sha256_batch, DFS_DEVICE_PTRS
     d_spans = torch.from_numpy(spans.view(np.int64).copy()).to(dev)
     d_dig = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
     d_st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     rc = sha256_static_device(eng, data.data_ptr(), d_spans.data_ptr(), n, d_dig.data_ptr(), d_st.data_ptr())
     assert rc == L.DFS_OK
     torch.cuda.synchronize(dev)
@@ -78,9 +80,11 @@ def test_static_entry_in_a_captured_graph():
     total = int(offs[-1] + lens[-1]) + 64
     gen = torch.Generator(device=dev).manual_seed(99)
     data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=gen)
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     d_spans = torch.from_numpy(spans.view(np.int64).copy()).to(dev)
     d_dig = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
     d_st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
     with dfs_amd.FragmentEngine(0) as eng, dfs_amd.FragmentEngine(0) as ref:
         s = torch.cuda.Stream(dev)
         eng.set_stream(s.cuda_stream)
