@@ -87,7 +87,13 @@ int dfs_open(dfs_ctx** ctx, int device);
 int dfs_close(dfs_ctx* ctx);
 const char* dfs_strerror(int code);
 int dfs_abi_version(void);
-/* Run subsequent calls on `hip_stream` (a hipStream_t; NULL = the ctx's own). */
+/* Run subsequent calls on `hip_stream` (a hipStream_t; NULL = the ctx's own).
+ * The ctx's own stream is non-blocking: it does not wait for the legacy
+ * default stream or for any other stream.  A DFS_DEVICE_PTRS caller whose own
+ * work fills or reads the buffers on another stream must order the two
+ * itself: hand that stream in here, or synchronise / use events around the
+ * call.  (Seen without it: a zero fill queued on the default stream just
+ * before an encode landed after it and wiped the encode's output.) */
 int dfs_set_stream(dfs_ctx* ctx, void* hip_stream);
 /* When on, every call records HIP events around each kernel on the stream it
  * is launched on; dfs_get_timings returns the last call's per-stage ms. */
