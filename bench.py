@@ -384,6 +384,7 @@ def download_leg(args, eng, files, plan, fd, frd, b64, S, N, F, dev, log):
     s_gat, s_rtot = [], []
     try:
         out.zero_()
+        torch.cuda.synchronize(dev)  # torch's stream; the library runs on the engine's
         reassemble_device(eng_s, addr, flen, F, N, out.data_ptr(), file_off, exp)
         eng_s.set_profiling(True)
         for _ in range(reps):
@@ -932,6 +933,7 @@ def multi_gpu(args, world, rank, local, log):
         pos = int(fr[k]["b64_off"]) + 5
         ch0["held"][pos] = ord("B") if int(ch0["held"][pos]) == ord("A") else ord("A")
         probe[0], probe[1] = k, int(fr[k]["rank"])
+        torch.cuda.synchronize(dev)  # the flipped char is in place before the library's stream reads it
     dist.broadcast(probe, src=0)
     probe = probe.cpu()  # the broadcast is complete before the library's own communicator is used again
     verify_only()
