@@ -8,7 +8,7 @@ cd "$(dirname "$0")/../distributed-file-storage_amd"
 mkdir -p build_checked
 FLAGS="-O2 -g1 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Xclang -target-feature -Xclang -packed-fp32-ops -D_GLIBCXX_ASSERTIONS"
 objs=""
-for f in csrc/sha256.hip csrc/base64.hip csrc/gather.hip csrc/dfs_gpu.cpp csrc/fragstore.cpp csrc/placement.cpp csrc/hostcomm.cpp csrc/replica.cpp csrc/batcher.cpp; do
+for f in csrc/sha256.hip csrc/base64.hip csrc/gather.hip csrc/dfs_gpu.cpp csrc/fragstore.cpp csrc/placement.cpp csrc/hostcomm.cpp csrc/replica.cpp csrc/batcher.cpp csrc/wire_host.cpp; do
   o=build_checked/$(basename $f).o
   /opt/rocm/bin/hipcc $FLAGS -x hip -c $f -o $o &
   objs="$objs $o"
