@@ -1065,6 +1065,8 @@ def multi_gpu(args, world, rank, local, log):
             "step_without_verify_ms": round(t_noverify * 1e3, 3),
             "receive_verify": {"held_fragments_per_gpu": held_frags, "decoded_bytes_per_gpu": raw_bytes,
                                "plan_ms": round(sh.replica_plan_ms, 2),
+                               "kernels": "one pass (each lane decodes, stores and hashes its fragment)"
+                               if sh.chunks[0]["rp"].one_pass else "decode kernel, then SHA-256 lanes",
                                "all_replicas_good": verify_ok, "corrupt_probe_caught": probe_ok,
                                "note": "inside the timed step: every rank's fragment digests to the holders "
                                        "(dfs_replica_exchange, RCCL), each holder Base64-decodes and SHA-256s every "

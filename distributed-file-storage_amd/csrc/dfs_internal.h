@@ -174,6 +174,18 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
                          int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr,
                          const ShaWait* wait = nullptr);
+// Held replicas in one pass (dfs_replica_check): lane i decodes the
+// 4 * ceil(n / 3) Base64 chars at in + src (dword aligned), writes the n decoded
+// bytes at raw + dst (16-byte aligned) and their SHA-256 at digests + 32 * out;
+// status[out] = bit 0 (a char outside the alphabet or a bad final unit) |
+// bit 1 (the decoded length is not n), as the decode kernel reports them.
+// Lanes sorted longest first keep the waves uniform.  `queue`: 64 words.
+struct DecLane {
+    uint64_t src, dst, n;
+    uint32_t out, pad;
+};
+hipError_t launch_sha256_b64dec(const char* in, const DecLane* lanes, uint32_t n, uint8_t* raw, uint8_t* digests,
+                                int32_t* status, uint32_t* queue, int waves_per_simd, hipStream_t s);
 // Allocation-free variant (dfs_sha256_batch_static): descriptors and queue
 // words live in a file-scope device array of sha256.hip, whose address on
 // `device` static_scratch_init resolves once (that device current; called by

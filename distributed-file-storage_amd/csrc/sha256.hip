@@ -829,6 +829,185 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
     }
 }
 
+// ---------------------------------------------------------------------------
+// Held replicas (dfs_replica_check): Base64 decode, the decoded bytes written
+// out, and their SHA-256 in ONE pass, one fragment per lane (SN:281-282).  The
+// separate decode kernel writes the raw bytes and the SHA lanes read them back;
+// here a lane reads its fragment's chars, decodes them in registers, stores the
+// 64 decoded bytes of each block and compresses them, so the raw bytes cross
+// HBM once (written) instead of twice.  Only canonical encodings of a known
+// length are taken (chars = 4 * ceil(n / 3), as the uploader's encoder writes
+// them, SN:636); a lane whose chars are not that reports it in `status` exactly
+// as the decode kernel does (bit 0: IllegalArgumentException case, bit 1:
+// decoded length differs from n).
+//
+// Block k of the decoded stream is bytes [64k, 64k + 64) = the 22 units (4
+// chars -> 3 bytes) from unit floor(64k / 3) on, starting ph = k mod 3 bytes
+// into the first.  Units are decoded through four 256-entry LDS tables (one
+// per char position, values pre-shifted, bit 31 = outside the alphabet), the
+// 17 big-endian words at unit-aligned byte offsets 0, 4, ... 64 are put
+// together with constant shifts, and one v_perm per word applies the phase
+// (and a second one gives the dword in memory order for the store).  Blocks
+// that reach into the final unit (the padded one) and the message tail go the
+// slow way: units decoded one at a time into the raw buffer, then hashed from
+// there like any message.
+__device__ __forceinline__ void dec_load(const uint32_t* __restrict__ p, uint32_t (&d)[22]) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint4 v = q[i];
+        d[4 * i + 0] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+    }
+    const uint2 w = *reinterpret_cast<const uint2*>(p + 20);
+    d[20] = w.x; d[21] = w.y;
+}
+
+__device__ __forceinline__ uint32_t dec_unit4(const uint32_t* __restrict__ lut, uint32_t w) {
+    return lut[w & 255u] | lut[256u + ((w >> 8) & 255u)] | lut[512u + ((w >> 16) & 255u)] | lut[768u + (w >> 24)];
+}
+
+// One block: chars d (22 units), phase ph -> schedule words W, stored to dst.
+__device__ __forceinline__ void dec_block(const uint32_t* __restrict__ lut, uint32_t (&d)[22], uint32_t ph,
+                                          uint32_t (&W)[16], uint8_t* __restrict__ dst, uint32_t& bad) {
+#pragma unroll
+    for (int j = 0; j < 22; ++j) {
+        d[j] = dec_unit4(lut, d[j]);
+        bad |= d[j];
+    }
+    uint32_t w0[17];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int a = (4 * i) / 3, r = (4 * i) % 3;
+        w0[i] = r == 0 ? (d[a] << 8) | (d[a + 1] >> 16) : r == 1 ? (d[a] << 16) | (d[a + 1] >> 8) : (d[a] << 24) | d[a + 1];
+    }
+    w0[16] = d[21] << 16;  // stream bytes 64, 65 (only a phase > 0 reaches them)
+    const uint32_t be = 0x07060504u - ph * 0x01010101u, le = 0x04050607u - ph * 0x01010101u;
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        W[i] = __builtin_amdgcn_perm(w0[i], w0[i + 1], be);
+        m[i] = __builtin_amdgcn_perm(w0[i], w0[i + 1], le);
+    }
+    uint4* o = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = make_uint4(m[4 * i], m[4 * i + 1], m[4 * i + 2], m[4 * i + 3]);
+}
+
+__global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __restrict__ in,
+                                                                  const DecLane* __restrict__ lanes, uint32_t n,
+                                                                  uint8_t* __restrict__ raw,
+                                                                  uint8_t* __restrict__ digests,
+                                                                  int32_t* __restrict__ status,
+                                                                  uint32_t* __restrict__ queue) {
+    __shared__ uint32_t lut[4 * 256];
+    for (uint32_t c = threadIdx.x; c < 256u; c += kShaBlock) {
+        uint32_t v = 0x80000000u;
+        if (c >= 'A' && c <= 'Z') v = c - 'A';
+        else if (c >= 'a' && c <= 'z') v = c - 'a' + 26u;
+        else if (c >= '0' && c <= '9') v = c - '0' + 52u;
+        else if (c == '+') v = 62u;
+        else if (c == '/') v = 63u;
+        const bool ok = v < 64u;
+        lut[c] = ok ? v << 18 : v;
+        lut[256u + c] = ok ? v << 12 : v;
+        lut[512u + c] = ok ? v << 6 : v;
+        lut[768u + c] = v;
+    }
+    __syncthreads();
+    const uint32_t nitems = (n + 63u) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(queue + 1, 1u);
+        item = __builtin_amdgcn_readfirstlane(item);
+        if (item >= nitems) break;
+        const uint32_t gid = item * 64u + lane;
+        if (gid >= n) continue;
+        const DecLane L = lanes[gid];
+        const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + L.src);
+        uint8_t* __restrict__ dst = raw + L.dst;
+        const uint64_t q = (L.n + 2) / 3;                     // units; the last one is the final (padded) unit
+        const uint64_t nfull = L.n >> 6;
+        const uint64_t body = q ? 3 * (q - 1) : 0;            // bytes of the units before the final one
+        const uint32_t kb = static_cast<uint32_t>(nfull < (body >> 6) ? nfull : (body >> 6));  // blocks of body units only
+        uint32_t st[8];
+        init_state(st);
+        uint32_t bad = 0;
+        if (kb) {
+            uint32_t A[22], B[22], W[16];
+            const uint32_t last = kb - 1u;
+            // unit index of block k's first unit: floor(64k / 3) = 21k + floor(k / 3)
+            dec_load(src, A);
+            uint32_t k = 0, ph = 0;
+            const uint32_t* p = src;  // block k's first unit
+            for (;;) {
+                const uint32_t* pn = p + 21 + (ph == 2u ? 1 : 0);
+                dec_load(k < last ? pn : p, B);
+                dec_block(lut, A, ph, W, dst + 64ull * k, bad);
+                compress(st, W);
+                if (++k >= kb) break;
+                p = pn;
+                ph = ph == 2u ? 0u : ph + 1u;
+                pn = p + 21 + (ph == 2u ? 1 : 0);
+                dec_load(k < last ? pn : p, A);
+                dec_block(lut, B, ph, W, dst + 64ull * k, bad);
+                compress(st, W);
+                if (++k >= kb) break;
+                p = pn;
+                ph = ph == 2u ? 0u : ph + 1u;
+            }
+        }
+        // The rest, unit by unit into the raw buffer: body units from the one
+        // holding byte 64 kb, then the final unit by the decoder's rules
+        // ("xxxx" | "xxx=" | "xx==", anything else is an error).
+        bool err = false;
+        uint64_t total = 0;
+        const uint64_t pos = 64ull * kb;
+        if (q) {
+            const uint8_t* __restrict__ ch8 = reinterpret_cast<const uint8_t*>(src);
+            for (uint64_t u = pos / 3; u + 1 < q; ++u) {
+                const uint32_t v = dec_unit4(lut, src[u]);
+                bad |= v;
+#pragma unroll
+                for (uint32_t t = 0; t < 3; ++t) {
+                    const uint64_t i = 3 * u + t;
+                    if (i >= pos) dst[i] = static_cast<uint8_t>(v >> (16 - 8 * t));
+                }
+            }
+            const uint64_t f = 4 * (q - 1);
+            const uint32_t c2 = ch8[f + 2], c3 = ch8[f + 3];
+            const uint32_t d0 = lut[768u + ch8[f]], d1 = lut[768u + ch8[f + 1]], d2 = lut[768u + c2], d3 = lut[768u + c3];
+            uint32_t fin = 0, val = 0;
+            if ((d0 | d1) >> 31) err = true;
+            else if (c2 == '=' && c3 == '=') { fin = 1; val = (d0 << 18) | (d1 << 12); }
+            else if (!(d2 >> 31) && c3 == '=') { fin = 2; val = (d0 << 18) | (d1 << 12) | (d2 << 6); }
+            else if (!((d2 | d3) >> 31)) { fin = 3; val = (d0 << 18) | (d1 << 12) | (d2 << 6) | d3; }
+            else err = true;
+            total = body + fin;
+            for (uint32_t t = 0; t < fin; ++t) {
+                const uint64_t i = body + t;
+                if (i >= pos && i < L.n) dst[i] = static_cast<uint8_t>(val >> (16 - 8 * t));
+            }
+        }
+        if (bad >> 31) err = true;
+        // what this lane wrote, read back by its own loads below
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        ShaDesc sd{};
+        sd.off = L.dst;
+        sd.len = sd.total = L.n;
+        const Msg m = msg_setup(raw, sd);
+        if (kb < m.nfull) plain_range(st, m, kb, m.nfull);
+        for (uint32_t tb = 0; tb < m.ntb; ++tb) {
+            uint32_t W[16];
+            tail_block(m, tb, W);
+            compress(st, W);
+        }
+        store_digest(st, L.out, ~0u, digests, digests);
+        status[L.out] = (err ? 1 : 0) | (!err && total != L.n ? 2 : 0);
+    }
+}
+
 #define DFS_SHA_ARGS                                                                                     \
     const uint8_t *__restrict__ base, const ShaDesc *__restrict__ descs, uint32_t n, uint32_t split,       \
         uint32_t n_long, uint32_t cap, uint8_t *__restrict__ out0, uint8_t *__restrict__ out1,             \
@@ -888,6 +1067,19 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
         hipLaunchKernelGGL(sha256_lanes, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap, out0,
                            out1, queue, state, nullptr, wt);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_sha256_b64dec(const char* in, const DecLane* lanes, uint32_t n, uint8_t* raw, uint8_t* digests,
+                                int32_t* status, uint32_t* queue, int waves_per_simd, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipError_t e = launch_fill_u32(queue, 64, 0u, s);
+    if (e != hipSuccess) return e;
+    const uint64_t items = (n + 63u) / 64u;
+    uint64_t waves = 1024ull * static_cast<uint64_t>(waves_per_simd < 1 ? 1 : waves_per_simd);
+    if (waves > items) waves = items;
+    hipLaunchKernelGGL(sha256_b64dec_lanes, dim3(static_cast<uint32_t>((waves + 3) / 4)), dim3(kShaBlock), 0, s, in, lanes,
+                       n, raw, digests, status, queue);
     return hipGetLastError();
 }
 

@@ -151,6 +151,7 @@ SIGNATURES = {
     "dfs_replica_layout": (_int, [_u32, _u32, _u32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "dfs_replica_plan_create": (_int, [_vp, _u32, _u32, _vp, _vp, _u32, _vp]),
     "dfs_replica_plan_info": (_int, [_vp, _vp, _vp, _vp, _vp]),
+    "dfs_replica_plan_one_pass": (_int, [_vp]),
     "dfs_replica_plan_frags": (_int, [_vp, _vp]),
     "dfs_replica_verify": (_int, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dfs_replica_exchange": (_int, [_vp, _u32, _vp, _vp]),

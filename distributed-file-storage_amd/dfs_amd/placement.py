@@ -292,6 +292,11 @@ class ReplicaPlan:
                                           self.table.ctypes.data), "dfs_replica_plan_info")
         self.nheld, self.held_bytes, self.raw_bytes = n.value, held.value, raw.value
 
+    @property
+    def one_pass(self) -> bool:
+        """True if the check decodes, stores and hashes in one kernel."""
+        return lib().dfs_replica_plan_one_pass(self._p) == 1
+
     def frags(self) -> np.ndarray:
         out = np.zeros(max(self.nheld, 1), dtype=L.HELD_FRAG_DTYPE)
         check(lib().dfs_replica_plan_frags(self._p, out.ctypes.data), "dfs_replica_plan_frags")

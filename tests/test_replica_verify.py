@@ -44,13 +44,15 @@ def _run(engine, lens, nfrag, align128, seed):
                 host=files.cpu().numpy(), offs=offs)
 
 
-@pytest.mark.parametrize("slices", [0, 3])
+# how the holders' check runs: "two" = decode kernel, then SHA lanes over the decoded bytes; "slices" = that in
+# three slices (DFS_REPLICA_SLICES), slice i hashed while slice i + 1 is decoded on the second stream; "fused" =
+# one pass, every lane decodes, stores and hashes its own fragment (DFS_REPLICA_FUSED=1)
+@pytest.mark.parametrize("how", ["two", "slices", "fused"])
 @pytest.mark.parametrize("align128", [False, True])
 @pytest.mark.parametrize("shape", ["ragged", "uniform-large"])
-def test_replica_verify_single_rank(engine, align128, shape, slices, monkeypatch):
-    """slices = 3: the check in three slices (DFS_REPLICA_SLICES; one by
-    default), slice i hashed while slice i + 1 is decoded on the second
-    stream."""
+def test_replica_verify_single_rank(engine, align128, shape, how, monkeypatch):
+    slices = 3 if how == "slices" else 0
+    monkeypatch.setenv("DFS_REPLICA_FUSED", "1" if how == "fused" else "0")
     if slices:
         monkeypatch.setenv("DFS_REPLICA_SLICES", str(slices))
     rng = np.random.default_rng(5 + align128)
@@ -74,7 +76,8 @@ def test_replica_verify_single_rank(engine, align128, shape, slices, monkeypatch
         verdict = torch.full((rp.nheld,), 99, dtype=torch.int32, device=dev)
         failed = torch.full((1,), 99, dtype=torch.int32, device=dev)
         torch.cuda.synchronize()  # torch filled these on its stream; the library runs on the engine's
-        print(f"replica verify {shape} align128={align128} slices={slices}: {rp.nheld} held fragments", flush=True)
+        assert rp.one_pass == (how == "fused")
+        print(f"replica verify {shape} align128={align128} {how}: {rp.nheld} held fragments", flush=True)
         rp.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
         torch.cuda.synchronize()
         assert int(failed[0]) == 0 and bool((verdict == 0).all())
@@ -134,4 +137,73 @@ def test_replica_verify_digest_is_the_oracles(engine):
     finally:
         c["rp"].close()
         c["comm"].close()
+        c["plan"].close()
+
+
+@pytest.mark.parametrize("align128", [False, True])
+def test_fused_check_every_length_and_final_unit_rule(engine, align128, monkeypatch):
+    """The one-pass check (a lane decodes, stores and hashes its fragment) on
+    fragments of every length 0..450 and a few long ones: block boundaries at
+    every phase of the 3-byte unit, tails of every size, final units "xxxx",
+    "xxx=" and "xx==".  Decoded bytes, digests and verdicts against the oracle;
+    then damaged replicas: a char outside the alphabet in the first block, in
+    the last whole block and in the final unit, padding where a char belongs and
+    a char where padding belongs (java.util.Base64's IllegalArgumentException,
+    SN:281, or a decoded length / digest that differs, SN:250-257) - each with
+    the verdict the two-kernel check gives for the same bytes."""
+    nfrag = 5
+    lens = [nfrag * n + r for n in range(0, 451, 3) for r in (0, 2)] + [nfrag * n for n in (1000, 4096, 4097, 65536 + 7)]
+    monkeypatch.setenv("DFS_REPLICA_FUSED", "1")
+    c = _run(engine, lens, nfrag, align128, 9100)
+    monkeypatch.setenv("DFS_REPLICA_FUSED", "0")
+    rp2 = P.ReplicaPlan(c["comm"], nfrag, lens, align128)
+    torch, dev, rp, comm = c["torch"], c["dev"], c["rp"], c["comm"]
+    assert rp.one_pass and not rp2.one_pass
+    try:
+        held = torch.zeros(max(rp.held_bytes, 1), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        comm.place("star", rp.table, c["b64"].data_ptr(), held.data_ptr())
+        torch.cuda.synchronize()
+        frags = rp.frags()
+
+        def run(plan):
+            raw = torch.full((plan.raw_bytes + 16,), 0xEE, dtype=torch.uint8, device=dev)
+            verdict = torch.full((plan.nheld,), 99, dtype=torch.int32, device=dev)
+            failed = torch.full((1,), 99, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            plan.verify(c["frd"].data_ptr(), held.data_ptr(), raw.data_ptr(), verdict.data_ptr(), failed.data_ptr())
+            torch.cuda.synchronize()
+            return raw.cpu().numpy(), verdict.cpu().numpy(), int(failed[0])
+
+        raw, v, failed = run(rp)
+        assert failed == 0 and not v.any()
+        for k, x in enumerate(frags):  # every decoded fragment, byte for byte (SN:281)
+            fo = int(c["offs"][int(x["file"])])
+            o, n = O.c_split(lens[int(x["file"])], nfrag)[int(x["frag"])]
+            a = int(x["raw_off"])
+            assert raw[a:a + n].tobytes() == c["host"][fo + o:fo + o + n].tobytes(), (k, n)
+            assert (raw[a + n:a + ((n + 15) & ~15)] == 0xEE).all(), (k, n)  # nothing written past the fragment
+        # damaged replicas: same verdicts from both checks
+        by_len = {}
+        for k, x in enumerate(frags):
+            by_len.setdefault(int(x["raw_len"]), k)
+        edits = []
+        for n, k in sorted(by_len.items()):
+            if n < 6:
+                continue
+            b0, bl = int(frags[k]["b64_off"]), int(frags[k]["b64_len"])
+            where = {0: 1, 1: bl - 6 if bl >= 12 else 2, 2: bl - 3, 3: bl - 1, 4: bl - 2}[len(edits) % 5]
+            newc = ord("=") if len(edits) % 5 == 3 else ord("!") if len(edits) % 5 < 3 else ord("A")
+            edits.append((b0 + where, newc))
+        for pos, ch in edits:
+            held[pos] = ch
+        torch.cuda.synchronize()
+        _, v1, f1 = run(rp)
+        _, v2, f2 = run(rp2)
+        assert f1 == f2 and f1 > 0 and v1.tolist() == v2.tolist()
+        assert set(np.unique(v1).tolist()) <= {0, L.DFS_E_DECODE, L.DFS_E_FRAG_MISMATCH} and L.DFS_E_DECODE in v1
+    finally:
+        rp2.close()
+        c["rp"].close()
+        comm.close()
         c["plan"].close()
