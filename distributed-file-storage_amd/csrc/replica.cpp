@@ -65,15 +65,12 @@ struct dfs_replica_plan {
     uint32_t* d_piece_rank = nullptr;
     uint32_t npieces = 0;
     // One-pass check (sha256_b64dec_lanes): every held fragment's chars are
-    // decoded, written and hashed by one lane.  An option (DFS_REPLICA_FUSED=1
-    // when the plan is made, one slice), not the default: on the 65,536 x
-    // 256 KiB / N = 8 chunk it takes 19.9 ms against 7.5 + 10.2 ms for the
-    // decode kernel and the SHA lanes.  Its VALU work is what was planned
-    // (+15 % per block), but a lane then issues ten 16-byte requests per block
-    // (six loads of chars, four stores of bytes) where a plain SHA lane issues
-    // five, every one to its own cache line, and the kernel stalls on issue
-    // (72 % of its wave cycles) while the decode kernel moves the same bytes
-    // in whole-line requests.  For 1 MiB / N = 5 fragments it is 7 % faster.
+    // decoded, written and hashed by one lane; the decoded bytes cross HBM once
+    // instead of twice.  The default from a mean fragment of 128 bytes up
+    // (DFS_REPLICA_FUSED=0 / 1 when the plan is made forces it off / on; one
+    // slice only): 14.6 against 7.5 + 10.2 ms on the 65,536 x 256 KiB / N = 8
+    // chunk, and ahead at every size tried from 128-byte to 210 KB fragments.
+    // The two-kernel check above stays for everything else.
     dfs::DecLane* d_lanes = nullptr;  // longest first
     bool fused = false;
 };
@@ -86,6 +83,9 @@ namespace {
     } while (0)
 
 uint64_t enc_len(uint64_t n) { return 4 * ((n + 2) / 3); }
+
+// Mean fragment length from which the one-pass check is taken by default.
+constexpr uint64_t kOnePassMinMean = 128;  // faster from 128-byte fragments up (measured); below: untried
 
 // Fragment f of a file of S bytes split into N (SN:138-141, 155).
 uint64_t frag_len(uint64_t S, uint32_t N, uint32_t f) { return S / N + (f < S % N ? 1 : 0); }
@@ -314,7 +314,9 @@ int dfs_replica_plan_create(dfs_comm* const* comms, uint32_t ncomms, uint32_t nf
             }
             std::vector<dfs::DecLane> lanes;
             if (!rc) {
-                p->fused = false;
+                uint64_t raw_total = 0;
+                for (const dfs_held_frag& h : L.frags) raw_total += h.raw_len;
+                p->fused = nslices == 1 && K && raw_total / K >= kOnePassMinMean;
                 if (const char* e = std::getenv("DFS_REPLICA_FUSED")) p->fused = nslices == 1 && K && e[0] == '1';
                 for (uint64_t k = 0; k < K && p->fused; ++k) {
                     const dfs_held_frag& h = L.frags[k];

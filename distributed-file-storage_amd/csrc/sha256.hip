@@ -19,6 +19,8 @@
 //  * Blocks are fetched in pairs (one 128-byte line for line-aligned
 //    messages) and the next pair is in flight while the current pair is
 //    compressed (four register buffers, loop unrolled x4).
+#include <cstdlib>
+
 #include "dfs_internal.h"
 
 namespace dfs {
@@ -318,9 +320,10 @@ __device__ __forceinline__ u32x4 enc_quad(const uint16_t* __restrict__ pair, con
 // fragment starts (DFS_LAYOUT_ALIGN128) every store is a full-line piece.
 template <int PH>
 __device__ __forceinline__ void enc_block(const uint16_t* __restrict__ pair, const uint32_t (&W)[16], uint32_t prev,
-                                          char* __restrict__ sb, uint32_t (&P)[21]) {
+                                          char* __restrict__ sb, uint32_t (&P)[21], bool EXP_nostore = false) {
     constexpr int F = PH == 0 ? 4 : (PH == 1 ? 3 : 2);
-    u32x4* d4 = reinterpret_cast<u32x4*>(sb);
+    u32x4 EXP_sink[16];
+    u32x4* d4 = EXP_nostore ? EXP_sink : reinterpret_cast<u32x4*>(sb);
     if (PH == 0) {
 #pragma unroll
         for (int q = 0; q < 5; ++q) {
@@ -365,6 +368,12 @@ __device__ __forceinline__ void enc_block(const uint16_t* __restrict__ pair, con
         d4[13] = u32x4{n2.z, n2.w, n3.x, n3.y};
         d4[14] = u32x4{n3.z, n3.w, n4.x, n4.y};
         d4[15] = u32x4{n4.z, n4.w, n20, n21};
+    }
+    if (EXP_nostore && PH) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = (PH == 1 ? 0 : 8); i < (PH == 1 ? 8 : 16); ++i) x ^= EXP_sink[i].x ^ EXP_sink[i].y ^ EXP_sink[i].z ^ EXP_sink[i].w;
+        if (x == 0x13572468u) *reinterpret_cast<uint32_t*>(sb) = x;
     }
 }
 
@@ -591,7 +600,7 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
         load_block(blk(bp, min(k + 1u, last)), m.sh, N, xn);                    \
         to_be(C, xc, m.sel);                                                      \
         if (enc && k < m.nfull) {                                                 \
-            enc_block<PH>(pair, C, prev, bdst, P);                                \
+            enc_block<PH>(pair, C, prev, bdst, P, W.ticks == 1);                  \
             prev = C[15];                                                         \
         }                                                                         \
         __builtin_amdgcn_sched_barrier(0); /* keep the encode out of the rounds */ \
@@ -833,9 +842,11 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
 // Held replicas (dfs_replica_check): Base64 decode, the decoded bytes written
 // out, and their SHA-256 in ONE pass, one fragment per lane (SN:281-282).  The
 // separate decode kernel writes the raw bytes and the SHA lanes read them back;
-// here a lane reads its fragment's chars, decodes them in registers, stores the
-// 64 decoded bytes of each block and compresses them, so the raw bytes cross
-// HBM once (written) instead of twice.  Only canonical encodings of a known
+// here a lane reads its fragment's chars, decodes them in registers, hands the
+// 64 decoded bytes of each block to the wave's staged store (DecTile: a lane's
+// own 16-byte stores to its own cache line cost the kernel a third of its time)
+// and compresses them, so the raw bytes cross HBM once (written) instead of
+// twice.  Only canonical encodings of a known
 // length are taken (chars = 4 * ceil(n / 3), as the uploader's encoder writes
 // them, SN:636); a lane whose chars are not that reports it in `status` exactly
 // as the decode kernel does (bit 0: IllegalArgumentException case, bit 1:
@@ -867,8 +878,19 @@ __device__ __forceinline__ uint32_t dec_unit4(const uint32_t* __restrict__ lut, 
 }
 
 // One block: chars d (22 units), phase ph -> schedule words W, stored to dst.
+// A wave's staging tile for its decoded blocks: lane l parks its 64 bytes in
+// v[l] (80-byte rows keep the 16-byte accesses off each other's banks), then
+// lanes 4i .. 4i+3 together write row i's 64 bytes to base[i] + the block's
+// offset, so one store instruction carries 16 whole 64-byte runs instead of 64
+// separate 16-byte pieces.
+struct DecTile {
+    uint4 v[64][5];
+    uint64_t base[64];
+};
+
 __device__ __forceinline__ void dec_block(const uint32_t* __restrict__ lut, uint32_t (&d)[22], uint32_t ph,
-                                          uint32_t (&W)[16], uint8_t* __restrict__ dst, uint32_t& bad) {
+                                          uint32_t (&W)[16], uint8_t* __restrict__ dst, uint64_t koff,
+                                          DecTile& tile, uint32_t& bad) {
 #pragma unroll
     for (int j = 0; j < 22; ++j) {
         d[j] = dec_unit4(lut, d[j]);
@@ -888,7 +910,25 @@ __device__ __forceinline__ void dec_block(const uint32_t* __restrict__ lut, uint
         W[i] = __builtin_amdgcn_perm(w0[i], w0[i + 1], be);
         m[i] = __builtin_amdgcn_perm(w0[i], w0[i + 1], le);
     }
-    uint4* o = reinterpret_cast<uint4*>(dst);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (__ballot(1) == ~0ull) {  // the whole wave is in this block together
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tile.v[lane][i] = make_uint4(m[4 * i], m[4 * i + 1], m[4 * i + 2], m[4 * i + 3]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t row = 16u * t + (lane >> 2), part = lane & 3u;
+            const uint4 q = tile.v[row][part];
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(tile.base[row]) + koff + 16u * part) = q;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        return;
+    }
+    uint4* o = reinterpret_cast<uint4*>(dst + koff);
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = make_uint4(m[4 * i], m[4 * i + 1], m[4 * i + 2], m[4 * i + 3]);
 }
@@ -900,6 +940,8 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
                                                                   int32_t* __restrict__ status,
                                                                   uint32_t* __restrict__ queue) {
     __shared__ uint32_t lut[4 * 256];
+    __shared__ DecTile tiles[kShaBlock / 64];
+    DecTile& tile = tiles[threadIdx.x >> 6];
     for (uint32_t c = threadIdx.x; c < 256u; c += kShaBlock) {
         uint32_t v = 0x80000000u;
         if (c >= 'A' && c <= 'Z') v = c - 'A';
@@ -926,6 +968,7 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
         const DecLane L = lanes[gid];
         const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + L.src);
         uint8_t* __restrict__ dst = raw + L.dst;
+        tile.base[lane] = reinterpret_cast<uint64_t>(dst);  // read by the wave's other lanes in dec_block, after its fences
         const uint64_t q = (L.n + 2) / 3;                     // units; the last one is the final (padded) unit
         const uint64_t nfull = L.n >> 6;
         const uint64_t body = q ? 3 * (q - 1) : 0;            // bytes of the units before the final one
@@ -943,14 +986,14 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
             for (;;) {
                 const uint32_t* pn = p + 21 + (ph == 2u ? 1 : 0);
                 dec_load(k < last ? pn : p, B);
-                dec_block(lut, A, ph, W, dst + 64ull * k, bad);
+                dec_block(lut, A, ph, W, dst, 64ull * k, tile, bad);
                 compress(st, W);
                 if (++k >= kb) break;
                 p = pn;
                 ph = ph == 2u ? 0u : ph + 1u;
                 pn = p + 21 + (ph == 2u ? 1 : 0);
                 dec_load(k < last ? pn : p, A);
-                dec_block(lut, B, ph, W, dst + 64ull * k, bad);
+                dec_block(lut, B, ph, W, dst, 64ull * k, tile, bad);
                 compress(st, W);
                 if (++k >= kb) break;
                 p = pn;
@@ -1058,8 +1101,10 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     if (waves > items && !n_long) waves = items;  // with long items the spare waves keep SIMDs balanced
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     if (b64) {
+        ShaWait ex{};
+        if (const char* e = std::getenv("DFS_ENC_EXPERIMENT")) ex.ticks = static_cast<uint64_t>(std::atoi(e));
         hipLaunchKernelGGL(sha256_lanes_b64, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
-                           out0, out1, queue, state, b64, ShaWait{});
+                           out0, out1, queue, state, b64, ex);
     } else if (wt.done) {
         hipLaunchKernelGGL(sha256_lanes_wait, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
                            out0, out1, queue, state, nullptr, wt);

@@ -660,10 +660,10 @@ int dfs_replica_plan_create(dfs_comm* const* comms, uint32_t ncomms, uint32_t nf
 int dfs_replica_plan_info(const dfs_replica_plan* plan, uint64_t* nheld, uint64_t* held_bytes, uint64_t* raw_bytes,
                           uint64_t* table);
 /* 1 if dfs_replica_check runs this plan in one pass (every lane decodes,
- * stores and hashes its own fragment; chosen with DFS_REPLICA_FUSED=1 in the
- * environment when the plan is made), 0 if it runs the decode kernel and then
- * the SHA-256 lanes (the default, and the faster one for 32 KiB fragments).
- * Same results either way. */
+ * stores and hashes its own fragment: the default for plans whose fragments
+ * average 128 bytes or more; DFS_REPLICA_FUSED=0 / 1 in the environment when
+ * the plan is made forces it off / on), 0 if it runs the decode kernel and
+ * then the SHA-256 lanes.  Same results either way. */
 int dfs_replica_plan_one_pass(const dfs_replica_plan* plan);
 int dfs_replica_plan_frags(const dfs_replica_plan* plan, dfs_held_frag* frags);
 /* Asynchronous on each comm's ctx stream; a plan runs one verify at a time.

@@ -5,7 +5,7 @@
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for shape in "" "--files 32768 --file-size 1048576 --nfrag 5"; do
+for shape in ""; do
   for rep in 1 2; do
     for fused in 1 0; do
       DFS_REPLICA_FUSED=$fused timeout -k 10 300 python -u bench.py --placement-step --no-cpu-baseline --steps 5 --warmup 1 $shape > gpurun_out/fc_$fused.json 2> gpurun_out/fc_$fused.err || { echo "run failed"; tail -5 gpurun_out/fc_$fused.err; exit 1; }

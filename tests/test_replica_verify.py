@@ -46,7 +46,7 @@ def _run(engine, lens, nfrag, align128, seed):
 
 # how the holders' check runs: "two" = decode kernel, then SHA lanes over the decoded bytes; "slices" = that in
 # three slices (DFS_REPLICA_SLICES), slice i hashed while slice i + 1 is decoded on the second stream; "fused" =
-# one pass, every lane decodes, stores and hashes its own fragment (DFS_REPLICA_FUSED=1)
+# one pass, every lane decodes, stores and hashes its own fragment (the default from 128-byte fragments up)
 @pytest.mark.parametrize("how", ["two", "slices", "fused"])
 @pytest.mark.parametrize("align128", [False, True])
 @pytest.mark.parametrize("shape", ["ragged", "uniform-large"])
