@@ -309,6 +309,48 @@ __device__ __forceinline__ u32x4 enc_quad(const uint16_t* __restrict__ pair, con
     return r;
 }
 
+// A wave's staging tile for 64-byte runs its lanes produce (decoded blocks,
+// halves of Base64 lines): lane l parks its 64 bytes in v[l] (80-byte rows keep
+// the 16-byte accesses off each other's banks), then lanes 4i .. 4i+3 together
+// write row i's 64 bytes to base[i] + the run's offset, so one store
+// instruction carries 16 whole 64-byte runs instead of 64 separate 16-byte
+// pieces (a lane's own 16-byte stores to its own cache line cost the one-pass
+// replica check a third of its time).  Wave-private: ordered by wavefront
+// fences, no barrier.
+struct DecTile {
+    uint4 v[64][5];
+    uint64_t base[64];
+};
+
+// Every lane of the wave calls this together (coop = the whole wave is here);
+// rows = ballot of the lanes whose q0..q3 are to be written at base[lane] + off.
+__device__ __forceinline__ void stage_store(DecTile& tile, bool coop, uint64_t rows, bool act, const uint4& q0,
+                                            const uint4& q1, const uint4& q2, const uint4& q3, uint64_t off) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (coop) {
+        if (act) {
+            tile.v[lane][0] = q0; tile.v[lane][1] = q1; tile.v[lane][2] = q2; tile.v[lane][3] = q3;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t row = 16u * t + (lane >> 2), part = lane & 3u;
+            if ((rows >> row) & 1ull) {
+                const uint4 q = tile.v[row][part];
+                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(tile.base[row]) + off + 16u * part) = q;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else if (act) {
+        uint4* o = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(tile.base[lane]) + off);
+        o[0] = q0; o[1] = q1; o[2] = q2; o[3] = q3;
+    }
+}
+
 // Block of phase PH (first group at X byte F = 4 - carry_in).  Output is
 // written in whole 128-byte lines of the 256-char super-block sb (3 blocks):
 // phase 0's 21 dwords wait in P, phase 1 writes line 0 (P[0..20] + its first
@@ -320,60 +362,68 @@ __device__ __forceinline__ u32x4 enc_quad(const uint16_t* __restrict__ pair, con
 // fragment starts (DFS_LAYOUT_ALIGN128) every store is a full-line piece.
 template <int PH>
 __device__ __forceinline__ void enc_block(const uint16_t* __restrict__ pair, const uint32_t (&W)[16], uint32_t prev,
-                                          char* __restrict__ sb, uint32_t (&P)[21], bool EXP_nostore = false) {
+                                          uint32_t (&P)[21], bool act, DecTile& tile, uint64_t off) {
     constexpr int F = PH == 0 ? 4 : (PH == 1 ? 3 : 2);
-    u32x4 EXP_sink[16];
-    u32x4* d4 = EXP_nostore ? EXP_sink : reinterpret_cast<u32x4*>(sb);
+    auto u4 = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return make_uint4(a, b, c, d); };
     if (PH == 0) {
+        if (act) {
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            const u32x4 v = q == 0 ? enc_quad<F, 0>(pair, W, prev)
-                          : q == 1 ? enc_quad<F, 4>(pair, W, prev)
-                          : q == 2 ? enc_quad<F, 8>(pair, W, prev)
-                          : q == 3 ? enc_quad<F, 12>(pair, W, prev)
-                                   : enc_quad<F, 16>(pair, W, prev);
-            P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
+            for (int q = 0; q < 5; ++q) {
+                const u32x4 v = q == 0 ? enc_quad<F, 0>(pair, W, prev)
+                              : q == 1 ? enc_quad<F, 4>(pair, W, prev)
+                              : q == 2 ? enc_quad<F, 8>(pair, W, prev)
+                              : q == 3 ? enc_quad<F, 12>(pair, W, prev)
+                                       : enc_quad<F, 16>(pair, W, prev);
+                P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
+            }
+            P[20] = enc_grp<F + 60>(pair, W, prev);
         }
-        P[20] = enc_grp<F + 60>(pair, W, prev);
-    } else if (PH == 1) {
-        const u32x4 n0 = enc_quad<F, 0>(pair, W, prev);
-        const u32x4 n1 = enc_quad<F, 4>(pair, W, prev);
-        const u32x4 n2 = enc_quad<F, 8>(pair, W, prev);
-        d4[0] = u32x4{P[0], P[1], P[2], P[3]};
-        d4[1] = u32x4{P[4], P[5], P[6], P[7]};
-        d4[2] = u32x4{P[8], P[9], P[10], P[11]};
-        d4[3] = u32x4{P[12], P[13], P[14], P[15]};
-        d4[4] = u32x4{P[16], P[17], P[18], P[19]};
-        d4[5] = u32x4{P[20], n0.x, n0.y, n0.z};
-        d4[6] = u32x4{n0.w, n1.x, n1.y, n1.z};
-        d4[7] = u32x4{n1.w, n2.x, n2.y, n2.z};
-        const u32x4 n3 = enc_quad<F, 12>(pair, W, prev);
-        const u32x4 n4 = enc_quad<F, 16>(pair, W, prev);
-        P[0] = n2.w;
-        P[1] = n3.x; P[2] = n3.y; P[3] = n3.z; P[4] = n3.w;
-        P[5] = n4.x; P[6] = n4.y; P[7] = n4.z; P[8] = n4.w;
-        P[9] = enc_grp<F + 60>(pair, W, prev);
-    } else {
-        const u32x4 n0 = enc_quad<F, 0>(pair, W, prev);
-        const u32x4 n1 = enc_quad<F, 4>(pair, W, prev);
-        const u32x4 n2 = enc_quad<F, 8>(pair, W, prev);
-        const u32x4 n3 = enc_quad<F, 12>(pair, W, prev);
-        const u32x4 n4 = enc_quad<F, 16>(pair, W, prev);
-        const uint32_t n20 = enc_grp<F + 60>(pair, W, prev), n21 = enc_grp<F + 63>(pair, W, prev);
-        d4[8] = u32x4{P[0], P[1], P[2], P[3]};
-        d4[9] = u32x4{P[4], P[5], P[6], P[7]};
-        d4[10] = u32x4{P[8], P[9], n0.x, n0.y};
-        d4[11] = u32x4{n0.z, n0.w, n1.x, n1.y};
-        d4[12] = u32x4{n1.z, n1.w, n2.x, n2.y};
-        d4[13] = u32x4{n2.z, n2.w, n3.x, n3.y};
-        d4[14] = u32x4{n3.z, n3.w, n4.x, n4.y};
-        d4[15] = u32x4{n4.z, n4.w, n20, n21};
+        return;
     }
-    if (EXP_nostore && PH) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int i = (PH == 1 ? 0 : 8); i < (PH == 1 ? 8 : 16); ++i) x ^= EXP_sink[i].x ^ EXP_sink[i].y ^ EXP_sink[i].z ^ EXP_sink[i].w;
-        if (x == 0x13572468u) *reinterpret_cast<uint32_t*>(sb) = x;
+    // Every lane of the wave's encode loop is here together (uniform trip
+    // count); act = this lane still has a block of its own to encode.
+    const bool coop = __ballot(1) == ~0ull;
+    const uint64_t rows = __ballot(act);
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
+    if (PH == 1) {  // line 0 of the super-block: P[0..20] + this block's first 11 dwords
+        if (act) {
+            q0 = u4(P[0], P[1], P[2], P[3]); q1 = u4(P[4], P[5], P[6], P[7]);
+            q2 = u4(P[8], P[9], P[10], P[11]); q3 = u4(P[12], P[13], P[14], P[15]);
+        }
+        stage_store(tile, coop, rows, act, q0, q1, q2, q3, off);
+        if (act) {
+            const u32x4 n0 = enc_quad<F, 0>(pair, W, prev);
+            const u32x4 n1 = enc_quad<F, 4>(pair, W, prev);
+            const u32x4 n2 = enc_quad<F, 8>(pair, W, prev);
+            q0 = u4(P[16], P[17], P[18], P[19]); q1 = u4(P[20], n0.x, n0.y, n0.z);
+            q2 = u4(n0.w, n1.x, n1.y, n1.z); q3 = u4(n1.w, n2.x, n2.y, n2.z);
+            const u32x4 n3 = enc_quad<F, 12>(pair, W, prev);
+            const u32x4 n4 = enc_quad<F, 16>(pair, W, prev);
+            P[0] = n2.w;
+            P[1] = n3.x; P[2] = n3.y; P[3] = n3.z; P[4] = n3.w;
+            P[5] = n4.x; P[6] = n4.y; P[7] = n4.z; P[8] = n4.w;
+            P[9] = enc_grp<F + 60>(pair, W, prev);
+        }
+        stage_store(tile, coop, rows, act, q0, q1, q2, q3, off + 64);
+    } else {  // line 1: P[0..9] + this block's 22 dwords
+        uint32_t c0 = 0, c1 = 0;  // n1.z, n1.w: the second half's first two dwords
+        if (act) {
+            const u32x4 n0 = enc_quad<F, 0>(pair, W, prev);
+            const u32x4 n1 = enc_quad<F, 4>(pair, W, prev);
+            q0 = u4(P[0], P[1], P[2], P[3]); q1 = u4(P[4], P[5], P[6], P[7]);
+            q2 = u4(P[8], P[9], n0.x, n0.y); q3 = u4(n0.z, n0.w, n1.x, n1.y);
+            c0 = n1.z; c1 = n1.w;
+        }
+        stage_store(tile, coop, rows, act, q0, q1, q2, q3, off + 128);
+        if (act) {
+            const u32x4 n2 = enc_quad<F, 8>(pair, W, prev);
+            const u32x4 n3 = enc_quad<F, 12>(pair, W, prev);
+            const u32x4 n4 = enc_quad<F, 16>(pair, W, prev);
+            const uint32_t n20 = enc_grp<F + 60>(pair, W, prev), n21 = enc_grp<F + 63>(pair, W, prev);
+            q0 = u4(c0, c1, n2.x, n2.y); q1 = u4(n2.z, n2.w, n3.x, n3.y);
+            q2 = u4(n3.z, n3.w, n4.x, n4.y); q3 = u4(n4.z, n4.w, n20, n21);
+        }
+        stage_store(tile, coop, rows, act, q0, q1, q2, q3, off + 192);
     }
 }
 
@@ -516,6 +566,8 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
     const uint32_t key = simd_key();
     __shared__ uint16_t pair[ENC ? 4096 : 2];           // Base64 character pairs
     __shared__ uint32_t stash[ENC ? 8 * kShaBlock : 1];  // states parked by finished lanes
+    __shared__ __align__(16) uint8_t tile_mem[ENC ? sizeof(DecTile) * (kShaBlock / 64) : 16];
+    DecTile& tile = reinterpret_cast<DecTile*>(tile_mem)[ENC ? threadIdx.x >> 6 : 0];
     if (ENC) {
         const uint8_t* a = reinterpret_cast<const uint8_t*>(kB64Alpha);
         for (uint32_t k = threadIdx.x; k < 4096u; k += kShaBlock)
@@ -581,6 +633,8 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
             if (ENC && (m.flags & kShaB64) != 0u) {
                 const bool enc = true;
                 char* bdst = b64 + descs[gid].b64;
+                tile.base[lane] = reinterpret_cast<uint64_t>(bdst);  // the wave's other lanes read it in stage_store
+                uint64_t boff = 0;                                   // the super-block's offset in every lane's output
                 if (kmax) {
                     // C holds block k, N receives block k+1 (clamped) while C
                     // is compressed; the body is unrolled over the three
@@ -599,9 +653,10 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
     {                                                                             \
         load_block(blk(bp, min(k + 1u, last)), m.sh, N, xn);                    \
         to_be(C, xc, m.sel);                                                      \
-        if (enc && k < m.nfull) {                                                 \
-            enc_block<PH>(pair, C, prev, bdst, P, W.ticks == 1);                  \
-            prev = C[15];                                                         \
+        {                                                                         \
+            const bool act = k < m.nfull;                                         \
+            enc_block<PH>(pair, C, prev, P, act, tile, boff);                     \
+            if (act) prev = C[15];                                                \
         }                                                                         \
         __builtin_amdgcn_sched_barrier(0); /* keep the encode out of the rounds */ \
         compress(st, C);                                                          \
@@ -615,7 +670,7 @@ __device__ __forceinline__ void sha256_body(const uint8_t* __restrict__ base, co
                         DFS_SHA_STEP(0)
                         DFS_SHA_STEP(1)
                         DFS_SHA_STEP(2)
-                        bdst += 256;
+                        boff += 256;
                     }
 #undef DFS_SHA_STEP
                     if (early) unpark(stash, st);
@@ -878,16 +933,6 @@ __device__ __forceinline__ uint32_t dec_unit4(const uint32_t* __restrict__ lut, 
 }
 
 // One block: chars d (22 units), phase ph -> schedule words W, stored to dst.
-// A wave's staging tile for its decoded blocks: lane l parks its 64 bytes in
-// v[l] (80-byte rows keep the 16-byte accesses off each other's banks), then
-// lanes 4i .. 4i+3 together write row i's 64 bytes to base[i] + the block's
-// offset, so one store instruction carries 16 whole 64-byte runs instead of 64
-// separate 16-byte pieces.
-struct DecTile {
-    uint4 v[64][5];
-    uint64_t base[64];
-};
-
 __device__ __forceinline__ void dec_block(const uint32_t* __restrict__ lut, uint32_t (&d)[22], uint32_t ph,
                                           uint32_t (&W)[16], uint8_t* __restrict__ dst, uint64_t koff,
                                           DecTile& tile, uint32_t& bad) {
@@ -1101,10 +1146,8 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
     if (waves > items && !n_long) waves = items;  // with long items the spare waves keep SIMDs balanced
     const uint32_t grid = static_cast<uint32_t>((waves + 3) / 4);
     if (b64) {
-        ShaWait ex{};
-        if (const char* e = std::getenv("DFS_ENC_EXPERIMENT")) ex.ticks = static_cast<uint64_t>(std::atoi(e));
         hipLaunchKernelGGL(sha256_lanes_b64, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
-                           out0, out1, queue, state, b64, ex);
+                           out0, out1, queue, state, b64, ShaWait{});
     } else if (wt.done) {
         hipLaunchKernelGGL(sha256_lanes_wait, dim3(grid), dim3(kShaBlock), 0, s, base, descs, n, split, n_long, cap,
                            out0, out1, queue, state, nullptr, wt);
