@@ -80,7 +80,9 @@ struct dfs_ctx {
     uint32_t b64_prio = 1;       // s_setprio of the encode waves beside SHA (DFS_B64_PRIO; profiles/r02c_knobs)
     uint32_t dec_prio = 1;       // decode waves at s_setprio 3 beside SHA (DFS_DEC_PRIO=0: 0)
     uint32_t dec_wgs = 1;        // decode workgroups per CU beside SHA (DFS_DEC_WGS)
+    bool recv_one_pass = true;   // dfs_receive_fragments_batch: one-pass kernel for big aligned batches (DFS_RECV_FUSED=0: never)
     uint64_t ovl_redo = 0;       // overlap downloads whose SHA launch was redone (a wait timed out)
+    uint64_t recv_one_pass_calls = 0;  // dfs_receive_fragments_batch calls that took the one-pass kernel
     uint64_t wait_ticks = dfs::kShaWaitTicks;  // bound of an in-kernel group wait (DFS_SHA_WAIT_TICKS)
     uint32_t wait_never = 0;     // test hook (DFS_SHA_WAIT_FORCE_TIMEOUT=1): the SHA lanes wait for one more
                                  // workgroup than the decode / gather grid has and give up after 10 us, so
@@ -499,6 +501,7 @@ int dfs_open(dfs_ctx** out, int device) {
     if (const char* w = std::getenv("DFS_B64_WGS")) c->b64_wgs = std::max(1, std::min(8, std::atoi(w)));
     if (const char* w = std::getenv("DFS_B64_PRIO")) c->b64_prio = static_cast<uint32_t>(std::atoi(w) & 3);
     if (const char* w = std::getenv("DFS_DEC_PRIO")) c->dec_prio = std::atoi(w) ? 1u : 0u;
+    if (const char* w = std::getenv("DFS_RECV_FUSED")) c->recv_one_pass = w[0] != '0';
     if (const char* w = std::getenv("DFS_DEC_WGS")) c->dec_wgs = static_cast<uint32_t>(std::max(1, std::min(8, std::atoi(w))));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = dfs::static_scratch_init(device);  // dfs_sha256_batch_static's device array
@@ -570,7 +573,8 @@ int dfs_get_timings(dfs_ctx* c, float* ms, int n) {
 int dfs_get_stats(dfs_ctx* c, uint64_t* out, int n) {
     if (!c || !out) return DFS_E_ARG;
     std::lock_guard<std::mutex> lk(c->mu);
-    for (int k = 0; k < n; ++k) out[k] = k == DFS_S_OVL_REDO ? c->ovl_redo : 0;
+    for (int k = 0; k < n; ++k)
+        out[k] = k == DFS_S_OVL_REDO ? c->ovl_redo : k == DFS_S_RECV_ONE_PASS ? c->recv_one_pass_calls : 0;
     return DFS_OK;
 }
 
@@ -712,10 +716,88 @@ int dfs_sha256_update_batch(dfs_ctx* c, const uint8_t* base, const dfs_span* par
 }
 
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+// dfs_receive_fragments_batch in one pass (sha256_b64dec_any_lanes: a lane
+// decodes, stores and hashes its message) for batches big enough for the
+// persistent kernel whose messages start on dword boundaries and decode to
+// 16-byte aligned places.  Returns 1 if the batch is not of that kind (the
+// caller then decodes and hashes with the two kernels), else the call's code.
+int receive_one_pass(dfs_ctx* c, const char* in, const dfs_span* msgs, uint32_t n, uint8_t* out,
+                     const uint64_t* out_off, uint64_t* out_len, uint8_t* digests, int32_t* status, uint32_t flags) {
+    if (n <= dfs::kChainMaxLanes || !c->recv_one_pass) return 1;
+    const bool dev = flags & DFS_DEVICE_PTRS;
+    uint64_t in_end = 0, out_end = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if ((msgs[i].off & 3u) || (out_off[i] & 15u) || msgs[i].len >= (kMaxMsg / 3) * 4) return 1;
+        in_end = std::max(in_end, msgs[i].off + msgs[i].len);
+        out_end = std::max(out_end, out_off[i] + dfs_b64_decoded_cap(msgs[i].len));
+    }
+    if ((in_end && !in) || (out_end && !out)) return DFS_E_ARG;
+    if (dev && ((reinterpret_cast<uintptr_t>(in) & 3u) || (reinterpret_cast<uintptr_t>(out) & 15u))) return 1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (int rc = enter(c)) return rc;
+    Timer tm(c);
+    hipStream_t s = c->stream();
+    Scratch scratch(c, s);
+    const char* d_in = in;
+    uint8_t* d_out = out;
+    if (!dev) {
+        if (int rc = put(c, B_DATA_IN, in, in_end, s)) return rc;
+        d_in = c->buf[B_DATA_IN].as<char>();
+        HIPC(c->buf[B_DATA_OUT].ensure(out_end));
+        d_out = c->buf[B_DATA_OUT].as<uint8_t>();
+    }
+    std::vector<dfs::DecLane> lanes(n);
+    for (uint32_t i = 0; i < n; ++i) lanes[i] = dfs::DecLane{msgs[i].off, out_off[i], ~0ull, msgs[i].len, i, 0};
+    std::stable_sort(lanes.begin(), lanes.end(), [](const dfs::DecLane& a, const dfs::DecLane& b) { return a.len > b.len; });
+    if (int rc = put(c, B_DESC, lanes.data(), lanes.size() * sizeof(dfs::DecLane), s)) return rc;
+    HIPC(c->buf[B_STATUS].ensure(4ull * n));
+    HIPC(c->buf[B_OUTLEN].ensure(8ull * n));
+    HIPC(c->buf[B_DIG1].ensure(32ull * n));
+    HIPC(c->buf[B_QUEUE].ensure(dfs::kShaQueueBytes));
+    ++c->recv_one_pass_calls;
+    tm.begin(DFS_T_TOTAL, s);
+    tm.begin(DFS_T_SHA, s);
+    HIPC(dfs::launch_sha256_b64dec(d_in, c->buf[B_DESC].as<dfs::DecLane>(), n, d_out, c->buf[B_DIG1].as<uint8_t>(),
+                                   c->buf[B_STATUS].as<int32_t>(), c->buf[B_QUEUE].as<uint32_t>(), c->sha_wps, s,
+                                   c->buf[B_OUTLEN].as<uint64_t>()));
+    tm.end(DFS_T_SHA, s);
+    tm.end(DFS_T_TOTAL, s);
+    std::vector<int32_t> st(n);
+    std::vector<uint8_t> dig(32ull * n);
+    HIPC(dfs::d2h(c, st.data(), c->buf[B_STATUS].p, 4ull * n, s));
+    HIPC(dfs::d2h(c, out_len, c->buf[B_OUTLEN].p, 8ull * n, s));
+    HIPC(dfs::d2h(c, dig.data(), c->buf[B_DIG1].p, 32ull * n, s));
+    if (!dev && out_end) HIPC(dfs::d2h(c, out, d_out, out_end, s));
+    HIPC(dfs::quiet_sync(c, s));
+    int rc = DFS_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        status[i] = st[i] ? DFS_E_DECODE : DFS_OK;
+        if (st[i]) {
+            out_len[i] = 0;
+            rc = DFS_E_DECODE;
+        } else {
+            std::memcpy(digests + 32ull * i, dig.data() + 32ull * i, 32);  // a failed message's digest stays untouched
+        }
+    }
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
 int dfs_receive_fragments_batch(dfs_ctx* c, const char* in, const dfs_span* msgs, uint32_t n, uint8_t* out,
                                 const uint64_t* out_off, uint64_t* out_len, uint8_t* digests, int32_t* status,
                                 uint32_t flags) {
-    if (!c || (n && (!digests || !out_len || !status))) return DFS_E_ARG;
+    if (!c || (n && (!msgs || !out_off || !digests || !out_len || !status))) return DFS_E_ARG;
+    {
+        const int one = receive_one_pass(c, in, msgs, n, out, out_off, out_len, digests, status, flags);
+        if (one != 1) return one;
+    }
     // Decode (SN:281); the decode call synchronises and fills out_len / status.
     int rc = dfs_b64_decode_batch(c, in, msgs, n, out, out_off, out_len, status, flags);
     if (rc != DFS_OK && rc != DFS_E_DECODE) return rc;
@@ -2039,7 +2121,8 @@ int dfs_store_bodies_receive(dfs_ctx* c, const char* bodies, const dfs_span* bod
     uint64_t end = 0, total = 0;
     for (uint32_t i = 0; i < n; ++i) {
         out_off[i] = total;
-        total += 3 * ((body_spans[i].len + 3) / 4);  // >= both decoded payloads
+        // >= both decoded payloads, the second one's start and the next slot's rounded up to 16 bytes
+        total += (3 * ((body_spans[i].len + 3) / 4) + 16 + 15) & ~15ull;
         end = std::max(end, body_spans[i].off + body_spans[i].len);
     }
     out_off[n] = total;
@@ -2084,7 +2167,7 @@ int dfs_store_bodies_receive(dfs_ctx* c, const char* bodies, const dfs_span* bod
         msgs.push_back(dfs_span{body_spans[i].off + p.off_a, p.len_a});
         dst.push_back(out_off[i]);
         msgs.push_back(dfs_span{body_spans[i].off + p.off_b, p.len_b});
-        dst.push_back(out_off[i] + dfs_b64_decoded_cap(p.len_a));
+        dst.push_back((out_off[i] + dfs_b64_decoded_cap(p.len_a) + 15) & ~15ull);
         frag_off[2 * i + 1] = dst.back();
         who.push_back(i);
     }

@@ -174,18 +174,24 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue,
                          int waves_per_simd, hipStream_t s, uint32_t* state = nullptr, char* b64 = nullptr,
                          const ShaWait* wait = nullptr);
-// Held replicas in one pass (dfs_replica_check): lane i decodes the
-// 4 * ceil(n / 3) Base64 chars at in + src (dword aligned), writes the n decoded
-// bytes at raw + dst (16-byte aligned) and their SHA-256 at digests + 32 * out;
-// status[out] = bit 0 (a char outside the alphabet or a bad final unit) |
-// bit 1 (the decoded length is not n), as the decode kernel reports them.
+// Base64 decode + SHA-256 in one pass, one message per lane (held replicas:
+// dfs_replica_check; received request bodies: dfs_receive_fragments_batch).
+// Lane i decodes the chars at in + src (dword aligned), writes the decoded
+// bytes at raw + dst (16-byte aligned) and their SHA-256 at digests + 32 * out.
+// out_len == nullptr: the decoded length n is known and the chars are the
+// encoder's 4 * ceil(n / 3) (len is ignored); status[out] = bit 0 (a char
+// outside the alphabet or a bad final unit) | bit 1 (the decoded length is not
+// n), as the decode kernel reports them.  out_len != nullptr: len chars of
+// unknown decoded length (n is ignored); status[out] = 0 / 1, out_len[out] =
+// decoded bytes (0 on error), a failed message's digest is not written.
 // Lanes sorted longest first keep the waves uniform.  `queue`: 64 words.
 struct DecLane {
-    uint64_t src, dst, n;
+    uint64_t src, dst, n, len;
     uint32_t out, pad;
 };
 hipError_t launch_sha256_b64dec(const char* in, const DecLane* lanes, uint32_t n, uint8_t* raw, uint8_t* digests,
-                                int32_t* status, uint32_t* queue, int waves_per_simd, hipStream_t s);
+                                int32_t* status, uint32_t* queue, int waves_per_simd, hipStream_t s,
+                                uint64_t* out_len = nullptr);
 // Allocation-free variant (dfs_sha256_batch_static): descriptors and queue
 // words live in a file-scope device array of sha256.hip, whose address on
 // `device` static_scratch_init resolves once (that device current; called by

@@ -327,7 +327,7 @@ int dfs_replica_plan_create(dfs_comm* const* comms, uint32_t ncomms, uint32_t nf
                     lanes.resize(K);
                     for (uint64_t k = 0; k < K; ++k) {
                         const dfs_held_frag& h = L.frags[k];
-                        lanes[k] = dfs::DecLane{h.b64_off, h.raw_off, h.raw_len, static_cast<uint32_t>(k), 0};
+                        lanes[k] = dfs::DecLane{h.b64_off, h.raw_off, h.raw_len, h.b64_len, static_cast<uint32_t>(k), 0};
                     }
                     std::stable_sort(lanes.begin(), lanes.end(),
                                      [](const dfs::DecLane& a, const dfs::DecLane& b) { return a.n > b.n; });

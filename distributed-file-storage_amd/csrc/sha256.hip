@@ -978,12 +978,17 @@ __device__ __forceinline__ void dec_block(const uint32_t* __restrict__ lut, uint
     for (int i = 0; i < 4; ++i) o[i] = make_uint4(m[4 * i], m[4 * i + 1], m[4 * i + 2], m[4 * i + 3]);
 }
 
-__global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __restrict__ in,
-                                                                  const DecLane* __restrict__ lanes, uint32_t n,
-                                                                  uint8_t* __restrict__ raw,
-                                                                  uint8_t* __restrict__ digests,
-                                                                  int32_t* __restrict__ status,
-                                                                  uint32_t* __restrict__ queue) {
+// KNOWN: the lane's decoded length n is given and its chars are the encoder's
+// 4 * ceil(n / 3) (held replicas; status bit 1 reports a decoded length that
+// is not n).  Otherwise (a received request body, SN:281) the length follows
+// from the chars: len chars = whole units plus a final unit of 2 or 3 chars,
+// or of 4 with padding; one dangling char is the decoder's error; out_len gets
+// the decoded length (0 on error) and a failed message's digest is not written.
+template <bool KNOWN>
+__device__ __forceinline__ void b64dec_body(const char* __restrict__ in, const DecLane* __restrict__ lanes, uint32_t n,
+                                            uint8_t* __restrict__ raw, uint8_t* __restrict__ digests,
+                                            int32_t* __restrict__ status, uint64_t* __restrict__ out_len,
+                                            uint32_t* __restrict__ queue) {
     __shared__ uint32_t lut[4 * 256];
     __shared__ DecTile tiles[kShaBlock / 64];
     DecTile& tile = tiles[threadIdx.x >> 6];
@@ -1012,11 +1017,38 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
         if (gid >= n) continue;
         const DecLane L = lanes[gid];
         const uint32_t* __restrict__ src = reinterpret_cast<const uint32_t*>(in + L.src);
+        const uint8_t* __restrict__ ch8 = reinterpret_cast<const uint8_t*>(src);
         uint8_t* __restrict__ dst = raw + L.dst;
         tile.base[lane] = reinterpret_cast<uint64_t>(dst);  // read by the wave's other lanes in dec_block, after its fences
-        const uint64_t q = (L.n + 2) / 3;                     // units; the last one is the final (padded) unit
-        const uint64_t nfull = L.n >> 6;
-        const uint64_t body = q ? 3 * (q - 1) : 0;            // bytes of the units before the final one
+        // Units of 4 chars -> 3 bytes; the last one is the final unit: 4 chars
+        // "xxxx" | "xxx=" | "xx==", or (unknown length only) 2 or 3 chars.
+        const uint32_t r = KNOWN ? 0u : static_cast<uint32_t>(L.len & 3u);
+        const uint64_t q = KNOWN ? (L.n + 2) / 3 : (L.len >> 2) + (r ? 1u : 0u);
+        const uint64_t body = q ? 3 * (q - 1) : 0;  // bytes of the units before the final one
+        bool err = !KNOWN && r == 1u;               // a dangling char
+        uint32_t fin = 0, val = 0;
+        if (q && !err) {
+            const uint64_t f = 4 * (q - 1);
+            const uint32_t d0 = lut[768u + ch8[f]], d1 = lut[768u + ch8[f + 1]];
+            if (r == 0u) {
+                const uint32_t c2 = ch8[f + 2], c3 = ch8[f + 3];
+                const uint32_t d2 = lut[768u + c2], d3 = lut[768u + c3];
+                if ((d0 | d1) >> 31) err = true;
+                else if (c2 == '=' && c3 == '=') { fin = 1; val = (d0 << 18) | (d1 << 12); }
+                else if (!(d2 >> 31) && c3 == '=') { fin = 2; val = (d0 << 18) | (d1 << 12) | (d2 << 6); }
+                else if (!((d2 | d3) >> 31)) { fin = 3; val = (d0 << 18) | (d1 << 12) | (d2 << 6) | d3; }
+                else err = true;
+            } else {
+                const uint32_t d2 = r == 3u ? lut[768u + ch8[f + 2]] : 0u;
+                if ((d0 | d1 | d2) >> 31) err = true;
+                fin = r - 1u;
+                val = (d0 << 18) | (d1 << 12) | (d2 << 6);
+            }
+        }
+        const uint64_t total = err ? 0 : body + fin;    // what the decoder returns
+        const uint64_t len = KNOWN ? L.n : total;       // bytes written and hashed
+        const bool skip = !KNOWN && err;                // nothing to decode: the request fails (SN:281)
+        const uint64_t nfull = len >> 6;
         const uint32_t kb = static_cast<uint32_t>(nfull < (body >> 6) ? nfull : (body >> 6));  // blocks of body units only
         uint32_t st[8];
         init_state(st);
@@ -1046,13 +1078,9 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
             }
         }
         // The rest, unit by unit into the raw buffer: body units from the one
-        // holding byte 64 kb, then the final unit by the decoder's rules
-        // ("xxxx" | "xxx=" | "xx==", anything else is an error).
-        bool err = false;
-        uint64_t total = 0;
+        // holding byte 64 kb, then the final unit's bytes.
         const uint64_t pos = 64ull * kb;
-        if (q) {
-            const uint8_t* __restrict__ ch8 = reinterpret_cast<const uint8_t*>(src);
+        if (q && !skip) {
             for (uint64_t u = pos / 3; u + 1 < q; ++u) {
                 const uint32_t v = dec_unit4(lut, src[u]);
                 bad |= v;
@@ -1062,19 +1090,9 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
                     if (i >= pos) dst[i] = static_cast<uint8_t>(v >> (16 - 8 * t));
                 }
             }
-            const uint64_t f = 4 * (q - 1);
-            const uint32_t c2 = ch8[f + 2], c3 = ch8[f + 3];
-            const uint32_t d0 = lut[768u + ch8[f]], d1 = lut[768u + ch8[f + 1]], d2 = lut[768u + c2], d3 = lut[768u + c3];
-            uint32_t fin = 0, val = 0;
-            if ((d0 | d1) >> 31) err = true;
-            else if (c2 == '=' && c3 == '=') { fin = 1; val = (d0 << 18) | (d1 << 12); }
-            else if (!(d2 >> 31) && c3 == '=') { fin = 2; val = (d0 << 18) | (d1 << 12) | (d2 << 6); }
-            else if (!((d2 | d3) >> 31)) { fin = 3; val = (d0 << 18) | (d1 << 12) | (d2 << 6) | d3; }
-            else err = true;
-            total = body + fin;
             for (uint32_t t = 0; t < fin; ++t) {
                 const uint64_t i = body + t;
-                if (i >= pos && i < L.n) dst[i] = static_cast<uint8_t>(val >> (16 - 8 * t));
+                if (i >= pos && i < len) dst[i] = static_cast<uint8_t>(val >> (16 - 8 * t));
             }
         }
         if (bad >> 31) err = true;
@@ -1083,7 +1101,7 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         ShaDesc sd{};
         sd.off = L.dst;
-        sd.len = sd.total = L.n;
+        sd.len = sd.total = len;
         const Msg m = msg_setup(raw, sd);
         if (kb < m.nfull) plain_range(st, m, kb, m.nfull);
         for (uint32_t tb = 0; tb < m.ntb; ++tb) {
@@ -1091,9 +1109,33 @@ __global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __r
             tail_block(m, tb, W);
             compress(st, W);
         }
-        store_digest(st, L.out, ~0u, digests, digests);
-        status[L.out] = (err ? 1 : 0) | (!err && total != L.n ? 2 : 0);
+        if (KNOWN) {
+            store_digest(st, L.out, ~0u, digests, digests);
+            status[L.out] = (err ? 1 : 0) | (!err && total != L.n ? 2 : 0);
+        } else {
+            if (!err) store_digest(st, L.out, ~0u, digests, digests);
+            status[L.out] = err ? 1 : 0;
+            out_len[L.out] = err ? 0 : total;
+        }
     }
+}
+
+__global__ __launch_bounds__(kShaBlock) void sha256_b64dec_lanes(const char* __restrict__ in,
+                                                                  const DecLane* __restrict__ lanes, uint32_t n,
+                                                                  uint8_t* __restrict__ raw,
+                                                                  uint8_t* __restrict__ digests,
+                                                                  int32_t* __restrict__ status,
+                                                                  uint32_t* __restrict__ queue) {
+    b64dec_body<true>(in, lanes, n, raw, digests, status, nullptr, queue);
+}
+__global__ __launch_bounds__(kShaBlock) void sha256_b64dec_any_lanes(const char* __restrict__ in,
+                                                                      const DecLane* __restrict__ lanes, uint32_t n,
+                                                                      uint8_t* __restrict__ raw,
+                                                                      uint8_t* __restrict__ digests,
+                                                                      int32_t* __restrict__ status,
+                                                                      uint64_t* __restrict__ out_len,
+                                                                      uint32_t* __restrict__ queue) {
+    b64dec_body<false>(in, lanes, n, raw, digests, status, out_len, queue);
 }
 
 #define DFS_SHA_ARGS                                                                                     \
@@ -1159,15 +1201,19 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
 }
 
 hipError_t launch_sha256_b64dec(const char* in, const DecLane* lanes, uint32_t n, uint8_t* raw, uint8_t* digests,
-                                int32_t* status, uint32_t* queue, int waves_per_simd, hipStream_t s) {
+                                int32_t* status, uint32_t* queue, int waves_per_simd, hipStream_t s, uint64_t* out_len) {
     if (n == 0) return hipSuccess;
     hipError_t e = launch_fill_u32(queue, 64, 0u, s);
     if (e != hipSuccess) return e;
     const uint64_t items = (n + 63u) / 64u;
     uint64_t waves = 1024ull * static_cast<uint64_t>(waves_per_simd < 1 ? 1 : waves_per_simd);
     if (waves > items) waves = items;
-    hipLaunchKernelGGL(sha256_b64dec_lanes, dim3(static_cast<uint32_t>((waves + 3) / 4)), dim3(kShaBlock), 0, s, in, lanes,
-                       n, raw, digests, status, queue);
+    const dim3 grid(static_cast<uint32_t>((waves + 3) / 4));
+    if (out_len)
+        hipLaunchKernelGGL(sha256_b64dec_any_lanes, grid, dim3(kShaBlock), 0, s, in, lanes, n, raw, digests, status, out_len,
+                           queue);
+    else
+        hipLaunchKernelGGL(sha256_b64dec_lanes, grid, dim3(kShaBlock), 0, s, in, lanes, n, raw, digests, status, queue);
     return hipGetLastError();
 }
 

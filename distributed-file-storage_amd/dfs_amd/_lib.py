@@ -48,7 +48,7 @@ DFS_PLACE_RING, DFS_PLACE_STAR, DFS_PLACE_FETCH = 0, 1, 2
 DFS_XFER_SEND, DFS_XFER_RECV, DFS_XFER_COPY = 0, 1, 2
 
 DFS_T_SHA, DFS_T_B64ENC, DFS_T_B64DEC, DFS_T_GATHER, DFS_T_TOTAL, DFS_T_COUNT = range(6)
-DFS_S_OVL_REDO, DFS_S_COUNT = range(2)
+DFS_S_OVL_REDO, DFS_S_RECV_ONE_PASS, DFS_S_COUNT = range(3)
 
 
 class dfs_span(ctypes.Structure):

@@ -119,10 +119,12 @@ class FragmentEngine:
 
     def stats(self) -> dict:
         """ctx counters (dfs_get_stats): ovl_redo = decode-ahead downloads
-        whose SHA launch was redone after an in-kernel wait timed out."""
+        whose SHA launch was redone after an in-kernel wait timed out;
+        recv_one_pass = dfs_receive_fragments_batch calls that decoded and
+        hashed in one pass."""
         v = (ctypes.c_uint64 * L.DFS_S_COUNT)()
         check(lib().dfs_get_stats(self._ctx, v, L.DFS_S_COUNT), "dfs_get_stats")
-        return {"ovl_redo": int(v[0])}
+        return {"ovl_redo": int(v[L.DFS_S_OVL_REDO]), "recv_one_pass": int(v[L.DFS_S_RECV_ONE_PASS])}
 
     # -- sha256Hex (SN:603-613) ----------------------------------------------
     def sha256(self, messages: Sequence[bytes]) -> List[bytes]:
@@ -290,7 +292,7 @@ class FragmentEngine:
         n = len(bodies)
         buf, spans = _pack(bodies)
         out_off = np.zeros(n + 1, dtype=np.uint64)
-        cap = sum(3 * ((len(b) + 3) // 4) for b in bodies)
+        cap = sum((3 * ((len(b) + 3) // 4) + 16 + 15) & ~15 for b in bodies)  # dfs_store_bodies_receive's slots
         out = np.zeros(max(cap, 1), dtype=np.uint8)
         idx = np.zeros(max(2 * n, 1), dtype=np.uint32)
         foff = np.zeros(max(2 * n, 1), dtype=np.uint64)
@@ -501,7 +503,10 @@ def store_receive_device(engine: "FragmentEngine", d_bodies: int, spans: np.ndar
 
 
 def store_receive_out_bytes(spans: np.ndarray) -> int:
-    return int(sum(3 * ((int(ln) + 3) // 4) for ln in np.asarray(spans)[:, 1]))
+    """Bytes dfs_store_bodies_receive needs in `out`: per body 3*ceil(len/4) +
+    16, rounded up to a multiple of 16 (both payloads decode to 16-byte
+    aligned places)."""
+    return int(sum((3 * ((int(ln) + 3) // 4) + 16 + 15) & ~15 for ln in np.asarray(spans)[:, 1]))
 
 
 class UploadPlan:

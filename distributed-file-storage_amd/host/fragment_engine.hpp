@@ -171,7 +171,7 @@ public:
                           std::vector<std::pair<int, std::pair<Bytes, std::string>>>& frags) {
         dfs_span sp{0, body.size()};
         std::vector<uint64_t> out_off(2), foff(2), flen(2);
-        Bytes out(3 * ((body.size() + 3) / 4) + 1);
+        Bytes out(((3 * ((body.size() + 3) / 4) + 16 + 15) & ~size_t(15)) + 1);  // dfs_store_bodies_receive's slot
         uint32_t idx[2];
         uint8_t dig[64];
         char ids[64];

@@ -110,7 +110,8 @@ int dfs_get_timings(dfs_ctx* ctx, float* ms, int n);
  * the decode because an in-kernel wait for a fragment group timed out (the
  * results are still exact; the call was slow). */
 #define DFS_S_OVL_REDO 0
-#define DFS_S_COUNT 1
+#define DFS_S_RECV_ONE_PASS 1 /* dfs_receive_fragments_batch calls that ran in one pass */
+#define DFS_S_COUNT 2
 int dfs_get_stats(dfs_ctx* ctx, uint64_t* out, int n);
 
 /* ---- pure host helpers (no device) ---------------------------------------- */
@@ -206,7 +207,12 @@ int dfs_b64_decode_batch(dfs_ctx* ctx, const char* in, const dfs_span* msgs, uin
  * SHA-256 the decoded bytes (SN:282); digests[32*i] is the hash the node
  * replies with (buildHashResponse, SN:644-655), which the sender compares
  * with its own (SN:248-257).  status[i] / out_len[i] as dfs_b64_decode_batch;
- * digests of failed messages are left untouched.  Synchronous. */
+ * digests of failed messages are left untouched.  Synchronous. 
+ * A batch of more than 32,768 messages whose chars start on 4-byte boundaries
+ * of `in` and decode to 16-byte aligned places of `out` is decoded and hashed
+ * in one pass, every message by one lane; other batches by the decode kernel
+ * followed by the SHA-256 lanes.  Same results; DFS_RECV_FUSED=0 at dfs_open
+ * keeps the two kernels. */
 int dfs_receive_fragments_batch(dfs_ctx* ctx, const char* in, const dfs_span* msgs, uint32_t n,
                                 uint8_t* out, const uint64_t* out_off, uint64_t* out_len, uint8_t* digests,
                                 int32_t* status, uint32_t flags);
@@ -309,8 +315,9 @@ int dfs_store_bodies_build(dfs_ctx* ctx, const uint8_t* files, const dfs_span* f
  *   file_ids[64i..]      the fileId string (64 chars, not NUL-terminated)
  *   frag_index[2i+q]     entry q's "index" (q = 0, 1), in body order
  *   out_off              n+1 entries filled by the library: body i's slot
- *                        in out (3*ceil(len/4) bytes; out_off[n] = bytes
- *                        needed)
+ *                        in out (3*ceil(len/4) + 16 bytes rounded up to a
+ *                        multiple of 16, so that both payloads decode to
+ *                        16-byte aligned places; out_off[n] = bytes needed)
  *   out + frag_off[2i+q] entry q's decoded bytes (frag_len[2i+q] of them);
  *                        digests[64i + 32q] their SHA-256,
  *                        the hashes of the reply (buildHashResponse, SN:644-655)

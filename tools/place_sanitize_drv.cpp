@@ -32,7 +32,7 @@ hipError_t launch_b64_decode(const char*, const StreamJob*, uint32_t, uint64_t, 
 hipError_t launch_sha256(const uint8_t*, const ShaDesc*, uint32_t, uint32_t, uint32_t, uint8_t*, uint8_t*, uint32_t*, int,
                          hipStream_t, uint32_t*, char*, const ShaWait*) { return hipSuccess; }
 hipError_t launch_sha256_b64dec(const char*, const DecLane*, uint32_t, uint8_t*, uint8_t*, int32_t*, uint32_t*, int,
-                                hipStream_t) { return hipSuccess; }
+                                hipStream_t, uint64_t*) { return hipSuccess; }
 }  // namespace dfs
 
 static int fail(const char* what, uint32_t W, uint32_t N) {
