@@ -510,6 +510,7 @@ def wire_leg(args, eng, files, fd, frd, S, N, F, dev, log):
             "hbm_gbs": round(moved / (ms / 1e3) / 1e9, 1), "hbm_frac": round(moved / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "ok": bool(ok), "receive_wall_ms": round(recv_ms, 3),
             "receive_body_gbs": round(R * body_bytes / (recv_ms / 1e3) / 1e9, 1), "receive_ok": rok,
+            "receive_one_pass_calls": eng.stats()["recv_one_pass"],
             "note": "bodies byte-identical to buildFragmentsJson (SN:629-642); hbm_gbs = raw fragment bytes read "
                     "+ body bytes written per second; receive = device parse + decode + SHA-256 of every entry "
                     "(synchronous call, wall clock incl. host job planning), digests == upload-time fragment "
