@@ -18,7 +18,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"sha256_lanes": "sha", "b64_encode_kernel": "b64enc", "b64_decode_kernel": "b64dec",
+KERNELS = {"sha256_b64dec": "sha_b64dec", "sha256_lanes": "sha", "b64_encode_kernel": "b64enc", "b64_decode_kernel": "b64dec",
            "gather_kernel": "gather", "synth_kernel": "synth"}
 
 
