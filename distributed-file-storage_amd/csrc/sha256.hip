@@ -829,6 +829,32 @@ __device__ __forceinline__ void helper_block(const Msg& m, uint32_t nb, uint32_t
     }
 }
 
+// Helper wave of the chain kernels: K + W of every block of message m (nb
+// blocks in all, kmax = the workgroup's longest) into kw[(k & 1)][..][lane],
+// one block ahead of the owner wave; raw blocks k+1 (R) and k+2 (Q) in flight
+// while block k+1 is expanded.
+__device__ __forceinline__ void helper_run(const Msg& m, bool live, uint32_t nb, uint32_t kmax, uint4 (*kw)[16 * 64],
+                                           uint32_t lane) {
+    const uint32_t* bp = (live && m.nfull) ? m.p : g_dummy_block;
+    const uint32_t last = (live && m.nfull) ? m.nfull - 1u : 0u;
+    const uint32_t sh = live ? m.sh : 0u;
+    uint32_t R[16], Q[16], xr, xq;
+    load_block(bp, sh, R, xr);
+    if (kmax) helper_block(m, nb, 0, R, xr, kw[0] + lane);
+    load_block(blk(bp, min(1u, last)), sh, R, xr);
+    __syncthreads();
+    for (uint32_t k = 0; k < kmax; ++k) {
+        if (k + 1 < kmax) {
+            load_block(blk(bp, min(k + 2u, last)), sh, Q, xq);
+            helper_block(m, nb, k + 1, R, xr, kw[(k + 1) & 1u] + lane);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) R[i] = Q[i];
+            xr = xq;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __restrict__ base,
                                                             const ShaDesc* __restrict__ descs, uint32_t n,
                                                             uint32_t split, uint8_t* __restrict__ out0,
@@ -871,25 +897,143 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
             }
         }
     } else {
-        // raw blocks k+1 (R) and k+2 (Q) in flight while block k+1 is expanded
-        const uint32_t* bp = (live && m.nfull) ? m.p : g_dummy_block;
-        const uint32_t last = (live && m.nfull) ? m.nfull - 1u : 0u;
-        const uint32_t sh = live ? m.sh : 0u;
-        uint32_t R[16], Q[16], xr, xq;
-        load_block(bp, sh, R, xr);
-        if (kmax) helper_block(m, nb, 0, R, xr, kw[0] + lane);
-        load_block(blk(bp, min(1u, last)), sh, R, xr);
-        __syncthreads();
-        for (uint32_t k = 0; k < kmax; ++k) {
-            if (k + 1 < kmax) {
-                load_block(blk(bp, min(k + 2u, last)), sh, Q, xq);
-                helper_block(m, nb, k + 1, R, xr, kw[(k + 1) & 1u] + lane);
+        helper_run(m, live, nb, kmax, kw, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pair-lane latency kernel: the owner wave's 14 ops per round are the critical
+// path of a chain, and half of them (Sigma0 + Maj on a, b, c) do not depend on
+// the other half (Sigma1 + Ch on e, f, g) within a round.  Here TWO lanes of
+// the owner wave share one message: the E lane keeps (e, f, g, h), the A lane
+// (a, b, c, d), both run the SAME instruction stream with per-lane rotate
+// counts (6, 11, 25 / 2, 13, 22) and one select bit turns Ch into Maj
+// (Maj(a, b, c) = Ch(a ^ c, b, c)), then three DPP adds exchange the round's
+// results between the partners: 10 VALU ops per round instead of 14, 32
+// messages per workgroup instead of 64 (the launches this kernel serves leave
+// most of the chip idle anyway).
+//
+// Lane layout: DPP bank masks enable whole banks of 4 lanes, so E lanes are
+// banks 0 and 2 of each row of 16 (lane & 4 == 0), A lanes banks 1 and 3, and
+// a lane's partner is lane ^ 4 (row_shl:4 / row_shr:4).  Message p of the
+// workgroup = lanes with ((lane >> 3) << 2 | (lane & 3)) == p; the helper
+// wave expands the schedule on both lanes of a pair (same loads, same values)
+// so an owner lane reads K + W at its own index.
+//
+// Hazards (VALU write -> DPP read of the same VGPR needs 2 wait states; the
+// compiler does not see inside asm): every DPP source here is either written
+// at least one round earlier, or separated by the s_nop in the same asm.
+constexpr uint32_t kChain2Msgs = 32;  // messages per workgroup
+
+__device__ __forceinline__ uint32_t pair_index(uint32_t lane) { return ((lane >> 3) << 2) | (lane & 3u); }
+
+// One round of the pair-lane owner wave as asm text (operands: %0..%3 the
+// four state registers, X0..X3 = the ones playing x0..x3 in this round; %4 = Z;
+// %5..%7 temporaries; %8..%10 rotate counts; %11 the Maj select mask; KN = K + W
+// of the round after this one):
+//   S = rotr(x0, s0) ^ rotr(x0, s1) ^ rotr(x0, s2)   E: Sigma1(e)     A: Sigma0(a)
+//   F = Ch(x0 ^ (x2 & m), x1, x2)                    E: Ch(e, f, g)   A: Maj(a, b, c)
+//   Y = S + F + Z                                    E: T1            A: T2
+//   E lanes: x3 = x3[partner] + Y       (e' = d + T1)
+//   E lanes: Z  = x2 + KN               (the next round's h is this round's g)
+//   A lanes: x3 = Y[partner] + Y        (a' = T1 + T2)
+// The Z update sits between the two exchanges: it gives Y its two wait states
+// before the DPP read.  Whole quads of rounds go into one asm statement: the
+// compiler pads every asm result it cannot see into with a wait state.
+#define DFS_PAIR_ROUND(X0, X1, X2, X3, KN)                                               \
+    "v_alignbit_b32 %5, " X0 ", " X0 ", %8\n\t"                                          \
+    "v_alignbit_b32 %6, " X0 ", " X0 ", %9\n\t"                                          \
+    "v_alignbit_b32 %7, " X0 ", " X0 ", %10\n\t"                                         \
+    "v_bitop3_b32 %5, %5, %6, %7 bitop3:0x96\n\t"                                        \
+    "v_bitop3_b32 %6, " X0 ", " X2 ", %11 bitop3:0x78\n\t"                               \
+    "v_bitop3_b32 %6, %6, " X1 ", " X2 " bitop3:0xca\n\t"                                \
+    "v_add3_u32 %5, %5, %6, %4\n\t"                                                      \
+    "v_add_u32_dpp " X3 ", " X3 ", %5 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"          \
+    "v_add_u32_dpp %4, " X2 ", " KN " quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n\t" \
+    "v_add_u32_dpp " X3 ", %5, %5 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+
+__device__ __forceinline__ void owner_block2(uint32_t (&st)[4], const uint4* __restrict__ kw, bool act, uint32_t s0,
+                                             uint32_t s1, uint32_t s2, uint32_t m) {
+    uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+    // x2 / x3 are DPP sources below and were just written by the previous
+    // block's state update: two wait states, and everything after depends on it.
+    asm volatile("s_nop 1" : "+v"(x2), "+v"(x3));
+    // K + W quads are fetched two ahead: a quad's asm statement takes the next
+    // quad's first word, so that quad must have landed by then as well (one
+    // ahead, every statement waited out a fresh LDS read: 29.0 vs 22.5 ms per
+    // 1 MiB chain).
+    uint4 q = kw[0], qn = kw[64];
+    uint32_t Z = 0;  // E lanes: h + K + W of the coming round; A lanes: 0
+    asm volatile("v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
+                 : "+v"(Z)
+                 : "v"(x3), "v"(q.x));
 #pragma unroll
-                for (int i = 0; i < 16; ++i) R[i] = Q[i];
-                xr = xq;
-            }
+    for (int t4 = 0; t4 < 16; ++t4) {
+        const uint4 cur = q;
+        q = qn;
+        if (t4 + 2 < 16) qn = kw[(t4 + 2) * 64];
+        // Four rounds; the registers' roles rotate and are back in place after
+        // the fourth.  The last operand is the next quad's first K + W (after
+        // the block's last round: any register, Z is not used again).
+        uint32_t r0, r1, r2;
+        asm volatile(DFS_PAIR_ROUND("%0", "%1", "%2", "%3", "%12")
+                     DFS_PAIR_ROUND("%3", "%0", "%1", "%2", "%13")
+                     DFS_PAIR_ROUND("%2", "%3", "%0", "%1", "%14")
+                     DFS_PAIR_ROUND("%1", "%2", "%3", "%0", "%15")
+                     : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(Z), "=&v"(r0), "=&v"(r1), "=&v"(r2)
+                     : "v"(s0), "v"(s1), "v"(s2), "v"(m), "v"(cur.y), "v"(cur.z), "v"(cur.w), "v"(q.x));
+    }
+    if (act) {
+        st[0] += x0; st[1] += x1; st[2] += x2; st[3] += x3;
+    }
+}
+#undef DFS_PAIR_ROUND
+
+__global__ __launch_bounds__(kChainBlock) void sha256_chain2(const uint8_t* __restrict__ base,
+                                                             const ShaDesc* __restrict__ descs, uint32_t n,
+                                                             uint32_t split, uint8_t* __restrict__ out0,
+                                                             uint8_t* __restrict__ out1, uint32_t* __restrict__ state) {
+    __shared__ uint4 kw[2][16 * 64];  // [slot][t/4][lane]: 32 KiB
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool owner = threadIdx.x < 64u;
+    const uint32_t gid = blockIdx.x * kChain2Msgs + pair_index(lane);
+    const bool live = gid < n;
+    Msg m{};
+    uint32_t nb = 0;
+    if (live) {
+        m = msg_setup(base, descs[gid]);
+        nb = m.nfull + ((m.flags & kShaPartial) ? 0u : m.ntb);
+    }
+    const uint32_t kmax = __builtin_amdgcn_readfirstlane(wave_max(nb));  // same in both waves
+    if (owner) {
+        const bool A = (lane & 4u) != 0u;  // (a, b, c, d) lane; else (e, f, g, h)
+        uint32_t st[4];
+        if (live && (m.flags & kShaResume)) {
+            const uint4 s = reinterpret_cast<const uint4*>(state + 8ull * m.out)[A ? 0 : 1];
+            st[0] = s.x; st[1] = s.y; st[2] = s.z; st[3] = s.w;
+        } else if (A) {
+            st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
+        } else {
+            st[0] = 0x510e527fu; st[1] = 0x9b05688cu; st[2] = 0x1f83d9abu; st[3] = 0x5be0cd19u;
+        }
+        const uint32_t s0 = A ? 2u : 6u, s1 = A ? 13u : 11u, s2 = A ? 22u : 25u, sel = A ? ~0u : 0u;
+        __syncthreads();  // block 0 staged
+        for (uint32_t k = 0; k < kmax; ++k) {
+            owner_block2(st, kw[k & 1u] + lane, k < nb, s0, s1, s2, sel);
             __syncthreads();
         }
+        if (live) {
+            if (m.flags & kShaPartial) {
+                reinterpret_cast<uint4*>(state + 8ull * m.out)[A ? 0 : 1] = make_uint4(st[0], st[1], st[2], st[3]);
+            } else {
+                uint8_t* dst = m.out < split ? out0 + 32ull * m.out : out1 + 32ull * (m.out - split);
+                reinterpret_cast<uint4*>(dst)[A ? 0 : 1] =
+                    make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                               __builtin_bswap32(st[3]));
+            }
+        }
+    } else {
+        helper_run(m, live, nb, kmax, kw, lane);
     }
 }
 
@@ -1160,6 +1304,29 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
 }
 #undef DFS_SHA_ARGS
 
+// Latency-bound launch (n <= kChainMaxLanes).  Up to kChain2MaxLanes messages
+// the pair-lane kernel (two owner lanes per message, 32 messages per
+// workgroup: at most 256 workgroups, one per CU — with two on a CU a 1 MiB
+// chain took 43.9 instead of 22.5 ms); above that the one-lane kernel, whose
+// 64 messages per workgroup keep the launch within one wave per SIMD.
+// DFS_SHA_CHAIN=1 forces the one-lane kernel (A/B measurements).
+constexpr uint32_t kChain2MaxLanes = kChainMaxLanes / 4;
+
+hipError_t launch_chain(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split, uint8_t* out0,
+                        uint8_t* out1, uint32_t* state, hipStream_t s) {
+    static const bool one_lane = [] {
+        const char* e = std::getenv("DFS_SHA_CHAIN");
+        return e && e[0] == '1';
+    }();
+    if (n <= kChain2MaxLanes && !one_lane)
+        hipLaunchKernelGGL(sha256_chain2, dim3((n + kChain2Msgs - 1u) / kChain2Msgs), dim3(kChainBlock), 0, s, base,
+                           descs, n, split, out0, out1, state);
+    else
+        hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, split, out0,
+                           out1, state);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 int sha_wait_vgprs() {
@@ -1171,11 +1338,8 @@ hipError_t launch_sha256(const uint8_t* base, const ShaDesc* descs, uint32_t n, 
                          uint32_t prio_lanes, uint8_t* out0, uint8_t* out1, uint32_t* queue, int waves_per_simd,
                          hipStream_t s, uint32_t* state, char* b64, const ShaWait* wait) {
     if (n == 0) return hipSuccess;
-    if (!b64 && !wait && n <= kChainMaxLanes) {  // latency-bound launch: owner + helper waves
-        hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, split, out0,
-                           out1, state);
-        return hipGetLastError();
-    }
+    if (!b64 && !wait && n <= kChainMaxLanes)  // latency-bound launch: owner + helper waves
+        return launch_chain(base, descs, n, split, out0, out1, state, s);
     const ShaWait wt = wait && !b64 ? *wait : ShaWait{};
     if (!wait) {  // with a wait the caller zeroed the queue before the decode it waits on
         hipError_t e = hipMemsetAsync(queue, 0, kShaQueueBytes, s);
@@ -1289,8 +1453,7 @@ hipError_t launch_sha256_static(int device, const uint8_t* base, const uint64_t*
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (n <= kChainMaxLanes) {
-        hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, n, out, out,
-                           nullptr);
+        return launch_chain(base, descs, n, n, out, out, nullptr, s);
     } else {  // unsorted lanes, no long items: every wave pulls from the short queue
         const uint64_t items = (n + 63u) / 64u;
         uint64_t waves = 1024ull * static_cast<uint64_t>(waves_per_simd < 1 ? 1 : waves_per_simd);

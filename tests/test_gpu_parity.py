@@ -698,7 +698,7 @@ def test_concurrent_handlers_share_one_ctx(engine):
 
 def test_sha256_both_kernels_large_and_small_launches(engine):
     """Launches up to dfs::kChainMaxLanes lanes run the owner/helper latency
-    kernel, larger ones the persistent throughput kernel: the same random
+    kernels, larger ones the persistent throughput kernel: the same random
     messages (every alignment, lengths around the padding boundaries) through
     both, against hashlib."""
     rng = np.random.default_rng(77)
@@ -718,6 +718,15 @@ def test_sha256_both_kernels_large_and_small_launches(engine):
     assert all(big[i].tobytes() == want[i] for i in range(n_big))
     small = engine.sha256_spans(buf, spans[:5000])
     assert all(small[i].tobytes() == want[i] for i in range(5000))
+    # Launches up to half of kChainMaxLanes take the pair-lane latency kernel
+    # (two owner lanes per message, 32 messages per workgroup), the rest of the
+    # range the one-lane kernel (64 per workgroup): one launch in the upper
+    # range, and message counts around the workgroup sizes.
+    mid = engine.sha256_spans(buf, spans[:20000])
+    assert all(mid[i].tobytes() == want[i] for i in range(20000))
+    for k in (1, 2, 31, 32, 33, 63, 64, 65, 16384, 16385):
+        got = engine.sha256_spans(buf, spans[100:100 + k])
+        assert all(got[i].tobytes() == want[100 + i] for i in range(k)), k
 
 
 @pytest.mark.parametrize("mode", ["overlap", "pipelined", "serial", "overlap-timeout"])
