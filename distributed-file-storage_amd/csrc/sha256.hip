@@ -855,14 +855,32 @@ __device__ __forceinline__ void helper_run(const Msg& m, bool live, uint32_t nb,
     }
 }
 
-__global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __restrict__ base,
-                                                            const ShaDesc* __restrict__ descs, uint32_t n,
-                                                            uint32_t split, uint8_t* __restrict__ out0,
-                                                            uint8_t* __restrict__ out1, uint32_t* __restrict__ state) {
-    __shared__ uint4 kw[2][16 * 64];  // [slot][t/4][lane]: 32 KiB
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool owner = threadIdx.x < 64u;
-    const uint32_t gid = blockIdx.x * 64u + lane;
+// Blocks the chain kernels run for message gid (0 past the launch's end).
+__device__ __forceinline__ uint32_t chain_blocks(const ShaDesc* __restrict__ descs, uint32_t n, uint32_t gid) {
+    if (gid >= n) return 0u;
+    const uint64_t len = descs[gid].len;
+    const uint32_t ntb = (static_cast<uint32_t>(len) & 63u) < 56u ? 1u : 2u;
+    return static_cast<uint32_t>(len >> 6) + ((descs[gid].flags & kShaPartial) ? 0u : ntb);
+}
+
+// PAIRS owner/helper wave pairs per workgroup (waves [0, PAIRS) own, waves
+// [PAIRS, 2 PAIRS) help): with two pairs a CU's four SIMDs each hold one wave
+// of ONE workgroup.  Two workgroups of one pair on a CU land on the same two
+// SIMDs, and two waves on a SIMD run these chains at nearly half the speed
+// (a 1 MiB chain: 45.4 instead of 29.4 ms at 32,768 messages).  Every wave
+// passes the same number of barriers: kmax is the workgroup's longest message.
+template <int PAIRS>
+__global__ __launch_bounds__(kChainBlock * PAIRS) void sha256_chain(const uint8_t* __restrict__ base,
+                                                                    const ShaDesc* __restrict__ descs, uint32_t n,
+                                                                    uint32_t split, uint8_t* __restrict__ out0,
+                                                                    uint8_t* __restrict__ out1,
+                                                                    uint32_t* __restrict__ state) {
+    __shared__ uint4 kws[PAIRS][2][16 * 64];  // [pair][slot][t/4][lane]: 32 KiB per pair
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const bool owner = wave < static_cast<uint32_t>(PAIRS);
+    const uint32_t pair = owner ? wave : wave - PAIRS;
+    uint4 (*kw)[16 * 64] = kws[pair];
+    const uint32_t gid = (blockIdx.x * PAIRS + pair) * 64u + lane;
     const bool live = gid < n;
     Msg m{};
     uint32_t nb = 0;
@@ -870,8 +888,10 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain(const uint8_t* __res
         m = msg_setup(base, descs[gid]);
         nb = m.nfull + ((m.flags & kShaPartial) ? 0u : m.ntb);
     }
-    // same count in both waves: they read the same descriptors
-    const uint32_t kmax = __builtin_amdgcn_readfirstlane(wave_max(nb));
+    uint32_t nbw = 0;
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p) nbw = max(nbw, chain_blocks(descs, n, (blockIdx.x * PAIRS + p) * 64u + lane));
+    const uint32_t kmax = __builtin_amdgcn_readfirstlane(wave_max(nbw));
     if (owner) {
         uint32_t st[8];
         if (live && (m.flags & kShaResume)) {
@@ -989,14 +1009,18 @@ __device__ __forceinline__ void owner_block2(uint32_t (&st)[4], const uint4* __r
 }
 #undef DFS_PAIR_ROUND
 
-__global__ __launch_bounds__(kChainBlock) void sha256_chain2(const uint8_t* __restrict__ base,
-                                                             const ShaDesc* __restrict__ descs, uint32_t n,
-                                                             uint32_t split, uint8_t* __restrict__ out0,
-                                                             uint8_t* __restrict__ out1, uint32_t* __restrict__ state) {
-    __shared__ uint4 kw[2][16 * 64];  // [slot][t/4][lane]: 32 KiB
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool owner = threadIdx.x < 64u;
-    const uint32_t gid = blockIdx.x * kChain2Msgs + pair_index(lane);
+template <int PAIRS>
+__global__ __launch_bounds__(kChainBlock * PAIRS) void sha256_chain2(const uint8_t* __restrict__ base,
+                                                                     const ShaDesc* __restrict__ descs, uint32_t n,
+                                                                     uint32_t split, uint8_t* __restrict__ out0,
+                                                                     uint8_t* __restrict__ out1,
+                                                                     uint32_t* __restrict__ state) {
+    __shared__ uint4 kws[PAIRS][2][16 * 64];  // [pair][slot][t/4][lane]: 32 KiB per pair
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const bool owner = wave < static_cast<uint32_t>(PAIRS);
+    const uint32_t pair = owner ? wave : wave - PAIRS;
+    uint4 (*kw)[16 * 64] = kws[pair];
+    const uint32_t gid = (blockIdx.x * PAIRS + pair) * kChain2Msgs + pair_index(lane);
     const bool live = gid < n;
     Msg m{};
     uint32_t nb = 0;
@@ -1004,7 +1028,11 @@ __global__ __launch_bounds__(kChainBlock) void sha256_chain2(const uint8_t* __re
         m = msg_setup(base, descs[gid]);
         nb = m.nfull + ((m.flags & kShaPartial) ? 0u : m.ntb);
     }
-    const uint32_t kmax = __builtin_amdgcn_readfirstlane(wave_max(nb));  // same in both waves
+    uint32_t nbw = 0;
+#pragma unroll
+    for (int p = 0; p < PAIRS; ++p)
+        nbw = max(nbw, chain_blocks(descs, n, (blockIdx.x * PAIRS + p) * kChain2Msgs + pair_index(lane)));
+    const uint32_t kmax = __builtin_amdgcn_readfirstlane(wave_max(nbw));  // same in every wave of the workgroup
     if (owner) {
         const bool A = (lane & 4u) != 0u;  // (a, b, c, d) lane; else (e, f, g, h)
         uint32_t st[4];
@@ -1305,12 +1333,11 @@ __global__ __launch_bounds__(kShaBlock) void sha256_lanes_b64(DFS_SHA_ARGS) {
 #undef DFS_SHA_ARGS
 
 // Latency-bound launch (n <= kChainMaxLanes).  Up to kChain2MaxLanes messages
-// the pair-lane kernel (two owner lanes per message, 32 messages per
-// workgroup: at most 256 workgroups, one per CU — with two on a CU a 1 MiB
-// chain took 43.9 instead of 22.5 ms); above that the one-lane kernel, whose
-// 64 messages per workgroup keep the launch within one wave per SIMD.
-// DFS_SHA_CHAIN=1 forces the one-lane kernel (A/B measurements).
-constexpr uint32_t kChain2MaxLanes = kChainMaxLanes / 4;
+// the pair-lane kernel (two owner lanes per message, 32 messages per owner
+// wave), above that the one-lane kernel (64 per owner wave): either way at
+// most one wave per SIMD.  DFS_SHA_CHAIN=1 forces the one-lane kernel (A/B
+// measurements).
+constexpr uint32_t kChain2MaxLanes = kChainMaxLanes / 2;
 
 hipError_t launch_chain(const uint8_t* base, const ShaDesc* descs, uint32_t n, uint32_t split, uint8_t* out0,
                         uint8_t* out1, uint32_t* state, hipStream_t s) {
@@ -1318,12 +1345,22 @@ hipError_t launch_chain(const uint8_t* base, const ShaDesc* descs, uint32_t n, u
         const char* e = std::getenv("DFS_SHA_CHAIN");
         return e && e[0] == '1';
     }();
-    if (n <= kChain2MaxLanes && !one_lane)
-        hipLaunchKernelGGL(sha256_chain2, dim3((n + kChain2Msgs - 1u) / kChain2Msgs), dim3(kChainBlock), 0, s, base,
-                           descs, n, split, out0, out1, state);
-    else
-        hipLaunchKernelGGL(sha256_chain, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, split, out0,
-                           out1, state);
+    // One wave pair per workgroup while that leaves at most one workgroup per
+    // CU (256 CUs), two pairs above.
+    if (n <= kChain2MaxLanes && !one_lane) {
+        if (n <= 256u * kChain2Msgs)
+            hipLaunchKernelGGL(sha256_chain2<1>, dim3((n + kChain2Msgs - 1u) / kChain2Msgs), dim3(kChainBlock), 0, s,
+                               base, descs, n, split, out0, out1, state);
+        else
+            hipLaunchKernelGGL(sha256_chain2<2>, dim3((n + 2u * kChain2Msgs - 1u) / (2u * kChain2Msgs)),
+                               dim3(2 * kChainBlock), 0, s, base, descs, n, split, out0, out1, state);
+    } else if (n <= 256u * 64u) {
+        hipLaunchKernelGGL(sha256_chain<1>, dim3((n + 63u) / 64u), dim3(kChainBlock), 0, s, base, descs, n, split,
+                           out0, out1, state);
+    } else {
+        hipLaunchKernelGGL(sha256_chain<2>, dim3((n + 127u) / 128u), dim3(2 * kChainBlock), 0, s, base, descs, n,
+                           split, out0, out1, state);
+    }
     return hipGetLastError();
 }
 

@@ -729,6 +729,47 @@ def test_sha256_both_kernels_large_and_small_launches(engine):
         assert all(got[i].tobytes() == want[100 + i] for i in range(k)), k
 
 
+_ONE_LANE_CHILD = r"""
+import hashlib, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "distributed-file-storage_amd"))
+import dfs_amd
+rng = np.random.default_rng(5)
+n = 700
+lens = rng.integers(0, 900, n)
+lens[:13] = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 129]
+buf = rng.integers(0, 256, int(lens.sum()) + 4 * n, dtype=np.uint8)
+offs, o = [], 0
+for i, ln in enumerate(lens):
+    o += i % 4
+    offs.append(o)
+    o += int(ln)
+spans = np.stack([np.array(offs, np.uint64), lens.astype(np.uint64)], axis=1)
+raw = buf.tobytes()
+eng = dfs_amd.FragmentEngine(0)
+for k in (1, 63, 64, 65, n):
+    got = eng.sha256_spans(buf, spans[:k])
+    assert all(got[i].tobytes() == hashlib.sha256(raw[a:a + int(m)]).digest() for i, (a, m) in enumerate(spans[:k])), k
+up = eng.upload([raw[:100003]], 5)
+assert up[0].file_id == hashlib.sha256(raw[:100003]).hexdigest()
+eng.close()
+print("one-lane ok")
+"""
+
+
+def test_sha256_one_lane_chain_kernel_forced():
+    """DFS_SHA_CHAIN=1 (read once per process) sends small launches to the
+    one-lane latency kernel, which otherwise only runs launches above half of
+    dfs::kChainMaxLanes: the same checks against hashlib in a child process."""
+    import subprocess
+    import sys
+    env = dict(os.environ, DFS_SHA_CHAIN="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _ONE_LANE_CHILD, root], capture_output=True, text=True, env=env,
+                       timeout=150)
+    assert r.returncode == 0 and "one-lane ok" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("mode", ["overlap", "pipelined", "serial", "overlap-timeout"])
 def test_download_overlapped_large_batch(engine, mode, monkeypatch):
     """A download above dfs::kChainMaxLanes SHA lanes.  6,000 files (36,000
