@@ -803,7 +803,8 @@ __device__ __forceinline__ void owner_block(uint32_t (&st)[8], const uint4* __re
 
 // K[t] + W[t] of block k of m (raw words r + look-ahead x for full blocks,
 // the padded tail for k < nb, zeros past the lane's own blocks) into
-// kw[t/4 * 64][t%4].
+// kw[t/4 * STRIDE][t%4].
+template <int STRIDE = 64>
 __device__ __forceinline__ void helper_block(const Msg& m, uint32_t nb, uint32_t k, uint32_t (&r)[16], uint32_t x,
                                              uint4* __restrict__ kw) {
     uint32_t W[16];
@@ -825,7 +826,7 @@ __device__ __forceinline__ void helper_block(const Msg& m, uint32_t nb, uint32_t
             asm volatile("" : "+v"(W[t & 15]));
         }
         o[t & 3] = kK[t] + W[t & 15];
-        if ((t & 3) == 3) kw[(t >> 2) * 64] = make_uint4(o[0], o[1], o[2], o[3]);
+        if ((t & 3) == 3) kw[(t >> 2) * STRIDE] = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
 
@@ -851,6 +852,38 @@ __device__ __forceinline__ void helper_run(const Msg& m, bool live, uint32_t nb,
             for (int i = 0; i < 16; ++i) R[i] = Q[i];
             xr = xq;
         }
+        __syncthreads();
+    }
+}
+
+// The pair-lane kernel's helper: TWO blocks ahead of the owner wave into three
+// slots of 16 x 32 quads (kw3[(k % 3)][t/4 * 32 + idx], idx = the message's
+// index in the wave; both lanes of a pair expand the same message and write
+// the same words), so the owner can fetch the next block's first quads before
+// the barrier that ends the current one.  Slot (k + 2) % 3 was last read by
+// the owner during block k - 1, i.e. before the barrier this write follows.
+__device__ __forceinline__ void helper_run3(const Msg& m, bool live, uint32_t nb, uint32_t kmax, uint4 (*kw3)[16 * 32],
+                                            uint32_t idx) {
+    const uint32_t* bp = (live && m.nfull) ? m.p : g_dummy_block;
+    const uint32_t last = (live && m.nfull) ? m.nfull - 1u : 0u;
+    const uint32_t sh = live ? m.sh : 0u;
+    uint32_t R[16], Q[16], xr, xq;
+    load_block(bp, sh, R, xr);
+    load_block(blk(bp, min(1u, last)), sh, Q, xq);
+    if (kmax) helper_block<32>(m, nb, 0, R, xr, kw3[0] + idx);
+    load_block(blk(bp, min(2u, last)), sh, R, xr);
+    if (kmax > 1) helper_block<32>(m, nb, 1, Q, xq, kw3[1] + idx);
+    __syncthreads();  // blocks 0 and 1 staged
+    uint32_t slot = 2;  // (k + 2) % 3
+    for (uint32_t k = 0; k < kmax; ++k) {
+        if (k + 2 < kmax) {
+            load_block(blk(bp, min(k + 3u, last)), sh, Q, xq);
+            helper_block<32>(m, nb, k + 2, R, xr, kw3[slot] + idx);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) R[i] = Q[i];
+            xr = xq;
+        }
+        slot = slot == 2u ? 0u : slot + 1u;
         __syncthreads();
     }
 }
@@ -972,26 +1005,30 @@ __device__ __forceinline__ uint32_t pair_index(uint32_t lane) { return ((lane >>
     "v_add_u32_dpp %4, " X2 ", " KN " quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n\t" \
     "v_add_u32_dpp " X3 ", %5, %5 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
 
-__device__ __forceinline__ void owner_block2(uint32_t (&st)[4], const uint4* __restrict__ kw, bool act, uint32_t s0,
+// kw: this block's K + W quads (kw[t/4 * 32]); nxt: the next block's (staged
+// two blocks ahead by the helper, so readable throughout this block).  q / qn
+// arrive holding this block's quads 0 and 1 and leave holding the next
+// block's: no LDS read waits behind the block's barrier.
+__device__ __forceinline__ void owner_block2(uint32_t (&st)[4], const uint4* __restrict__ kw,
+                                             const uint4* __restrict__ nxt, uint4& q, uint4& qn, bool act, uint32_t s0,
                                              uint32_t s1, uint32_t s2, uint32_t m) {
     uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
     // x2 / x3 are DPP sources below and were just written by the previous
     // block's state update: two wait states, and everything after depends on it.
     asm volatile("s_nop 1" : "+v"(x2), "+v"(x3));
-    // K + W quads are fetched two ahead: a quad's asm statement takes the next
-    // quad's first word, so that quad must have landed by then as well (one
-    // ahead, every statement waited out a fresh LDS read: 29.0 vs 22.5 ms per
-    // 1 MiB chain).
-    uint4 q = kw[0], qn = kw[64];
     uint32_t Z = 0;  // E lanes: h + K + W of the coming round; A lanes: 0
     asm volatile("v_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
                  : "+v"(Z)
                  : "v"(x3), "v"(q.x));
+    // K + W quads are fetched two ahead: a quad's asm statement takes the next
+    // quad's first word, so that quad must have landed by then as well (one
+    // ahead, every statement waited out a fresh LDS read: 29.0 vs 22.5 ms per
+    // 1 MiB chain).
 #pragma unroll
     for (int t4 = 0; t4 < 16; ++t4) {
         const uint4 cur = q;
         q = qn;
-        if (t4 + 2 < 16) qn = kw[(t4 + 2) * 64];
+        qn = t4 + 2 < 16 ? kw[(t4 + 2) * 32] : nxt[(t4 - 14) * 32];
         // Four rounds; the registers' roles rotate and are back in place after
         // the fourth.  The last operand is the next quad's first K + W (after
         // the block's last round: any register, Z is not used again).
@@ -1015,12 +1052,13 @@ __global__ __launch_bounds__(kChainBlock * PAIRS) void sha256_chain2(const uint8
                                                                      uint32_t split, uint8_t* __restrict__ out0,
                                                                      uint8_t* __restrict__ out1,
                                                                      uint32_t* __restrict__ state) {
-    __shared__ uint4 kws[PAIRS][2][16 * 64];  // [pair][slot][t/4][lane]: 32 KiB per pair
+    __shared__ uint4 kws[PAIRS][3][16 * 32];  // [pair][slot][t/4][message]: 24 KiB per pair
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const bool owner = wave < static_cast<uint32_t>(PAIRS);
     const uint32_t pair = owner ? wave : wave - PAIRS;
-    uint4 (*kw)[16 * 64] = kws[pair];
-    const uint32_t gid = (blockIdx.x * PAIRS + pair) * kChain2Msgs + pair_index(lane);
+    uint4 (*kw)[16 * 32] = kws[pair];
+    const uint32_t idx = pair_index(lane);
+    const uint32_t gid = (blockIdx.x * PAIRS + pair) * kChain2Msgs + idx;
     const bool live = gid < n;
     Msg m{};
     uint32_t nb = 0;
@@ -1045,9 +1083,13 @@ __global__ __launch_bounds__(kChainBlock * PAIRS) void sha256_chain2(const uint8
             st[0] = 0x510e527fu; st[1] = 0x9b05688cu; st[2] = 0x1f83d9abu; st[3] = 0x5be0cd19u;
         }
         const uint32_t s0 = A ? 2u : 6u, s1 = A ? 13u : 11u, s2 = A ? 22u : 25u, sel = A ? ~0u : 0u;
-        __syncthreads();  // block 0 staged
+        __syncthreads();  // blocks 0 and 1 staged
+        uint4 q = kw[0][idx], qn = kw[0][32 + idx];
+        uint32_t slot = 0;  // k % 3
         for (uint32_t k = 0; k < kmax; ++k) {
-            owner_block2(st, kw[k & 1u] + lane, k < nb, s0, s1, s2, sel);
+            const uint32_t ns = slot == 2u ? 0u : slot + 1u;
+            owner_block2(st, kw[slot] + idx, kw[ns] + idx, q, qn, k < nb, s0, s1, s2, sel);
+            slot = ns;
             __syncthreads();
         }
         if (live) {
@@ -1061,7 +1103,7 @@ __global__ __launch_bounds__(kChainBlock * PAIRS) void sha256_chain2(const uint8
             }
         }
     } else {
-        helper_run(m, live, nb, kmax, kw, lane);
+        helper_run3(m, live, nb, kmax, kw, idx);
     }
 }
 
