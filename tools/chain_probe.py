@@ -1,8 +1,10 @@
 """Latency-bound SHA launches: time dfs_sha256_batch over n equal messages
-(device memory) for a sweep of n.  The library picks the owner/helper chain
-kernel up to dfs::kChainMaxLanes lanes and the persistent kernel above;
-profiles/r02_chain_vs_persistent.txt was measured with a temporary build
-whose threshold came from a DFS_CHAIN_MAX variable (not in the library)."""
+(device memory) for a sweep of n.  The library picks the pair-lane latency
+kernel up to half of dfs::kChainMaxLanes messages (DFS_SHA_CHAIN=1: the
+one-lane kernel there too), the one-lane kernel up to kChainMaxLanes and the
+persistent kernel above; profiles/r02_chain_vs_persistent.txt was measured
+with a temporary build whose threshold came from a DFS_CHAIN_MAX variable
+(not in the library)."""
 import os
 import sys
 import time
@@ -31,5 +33,5 @@ for n in counts:
         sha256_device(eng, buf.data_ptr(), spans[:n])
         ts.append(time.perf_counter() - t0)
     res[n] = round(min(ts) * 1e3, 2)
-    print(f"chain_max={os.environ.get('DFS_CHAIN_MAX', 'default')} n={n} S={S}: {res[n]} ms", flush=True)
+    print(f"one_lane={os.environ.get('DFS_SHA_CHAIN', '0')} n={n} S={S}: {res[n]} ms", flush=True)
 eng.close()
