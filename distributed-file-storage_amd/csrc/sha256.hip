@@ -963,20 +963,21 @@ __global__ __launch_bounds__(kChainBlock * PAIRS) void sha256_chain(const uint8_
 // counts (6, 11, 25 / 2, 13, 22) and one select bit turns Ch into Maj
 // (Maj(a, b, c) = Ch(a ^ c, b, c)), then three DPP adds exchange the round's
 // results between the partners: 10 VALU ops per round instead of 14, 32
-// messages per workgroup instead of 64 (the launches this kernel serves leave
-// most of the chip idle anyway).
+// messages per owner wave instead of 64 (the launches this kernel serves
+// leave most of the chip idle anyway).
 //
 // Lane layout: DPP bank masks enable whole banks of 4 lanes, so E lanes are
 // banks 0 and 2 of each row of 16 (lane & 4 == 0), A lanes banks 1 and 3, and
 // a lane's partner is lane ^ 4 (row_shl:4 / row_shr:4).  Message p of the
-// workgroup = lanes with ((lane >> 3) << 2 | (lane & 3)) == p; the helper
-// wave expands the schedule on both lanes of a pair (same loads, same values)
-// so an owner lane reads K + W at its own index.
+// wave = lanes with ((lane >> 3) << 2 | (lane & 3)) == p; the helper wave
+// expands the schedule on both lanes of a pair (same loads, same values,
+// written to the message's one place in LDS).
 //
 // Hazards (VALU write -> DPP read of the same VGPR needs 2 wait states; the
-// compiler does not see inside asm): every DPP source here is either written
-// at least one round earlier, or separated by the s_nop in the same asm.
-constexpr uint32_t kChain2Msgs = 32;  // messages per workgroup
+// compiler does not see inside asm): every DPP source here is written at
+// least one round earlier, or two instructions earlier inside the same asm
+// statement, or by the s_nop statement that opens a block.
+constexpr uint32_t kChain2Msgs = 32;  // messages per owner wave
 
 __device__ __forceinline__ uint32_t pair_index(uint32_t lane) { return ((lane >> 3) << 2) | (lane & 3u); }
 
