@@ -4,6 +4,7 @@ independent chains with explicit registers: every source in the destination's
 bank ("same") against sources spread over three banks ("spread"), at 8 waves
 per SIMD and at one.  Timing only.
   python3 tools/gen_vgpr_bank_probe.py && hipcc -O3 --offload-arch=gfx950 \
+      -Xclang -target-feature -Xclang -packed-fp32-ops \
       tools/vgpr_bank_probe.hip -o tools/vgpr_bank_probe && tools/vgpr_bank_probe"""
 import os
 
