@@ -95,3 +95,22 @@ def test_synth_fill_at_matches_oracle(engine):
         h = buf.cpu().numpy().tobytes()
         for f, (o, n) in enumerate(spans):
             assert h[int(o):int(o + n)] == O.c_synth(7 + f, off, int(n)), (off, f)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [9000, 20000])
+def test_sha256_update_many_messages_in_parts(engine, n):
+    """dfs_sha256_update_batch over thousands of messages in three parts (the
+    first two multiples of 64 bytes, states carried in HBM between launches):
+    9,000 messages run the pair-lane latency kernel with two wave pairs per
+    workgroup, 20,000 the one-lane kernel with two pairs; against hashlib."""
+    rng = np.random.default_rng(n)
+    cuts = [(64 * int(a), 64 * int(b), int(c)) for a, b, c in
+            zip(rng.integers(1, 4, n), rng.integers(0, 3, n), rng.integers(0, 130, n))]
+    msgs = [rng.integers(0, 256, a + b + c, dtype=np.uint8).tobytes() for a, b, c in cuts]
+    state = np.zeros((n, 8), dtype=np.uint32)
+    total = [len(m) for m in msgs]
+    assert engine.sha256_update([m[:a] for m, (a, b, c) in zip(msgs, cuts)], state, True, False) is None
+    assert engine.sha256_update([m[a:a + b] for m, (a, b, c) in zip(msgs, cuts)], state, False, False) is None
+    got = engine.sha256_update([m[a + b:] for m, (a, b, c) in zip(msgs, cuts)], state, False, True, total)
+    assert all(bytes(g) == hashlib.sha256(m).digest() for g, m in zip(got, msgs))
