@@ -898,10 +898,11 @@ __device__ __forceinline__ uint32_t chain_blocks(const ShaDesc* __restrict__ des
 
 // PAIRS owner/helper wave pairs per workgroup (waves [0, PAIRS) own, waves
 // [PAIRS, 2 PAIRS) help): with two pairs a CU's four SIMDs each hold one wave
-// of ONE workgroup.  Two workgroups of one pair on a CU land on the same two
-// SIMDs, and two waves on a SIMD run these chains at nearly half the speed
-// (a 1 MiB chain: 45.4 instead of 29.4 ms at 32,768 messages).  Every wave
-// passes the same number of barriers: kmax is the workgroup's longest message.
+// of ONE workgroup.  Two workgroups of one pair on a CU put two of their four
+// waves on one SIMD and leave another SIMD idle (tools/wave_place_probe), and
+// two waves on a SIMD run these chains at nearly half the speed (a 1 MiB
+// chain: 45.4 instead of 29.4 ms at 32,768 messages).  Every wave passes the
+// same number of barriers: kmax is the workgroup's longest message.
 template <int PAIRS>
 __global__ __launch_bounds__(kChainBlock * PAIRS) void sha256_chain(const uint8_t* __restrict__ base,
                                                                     const ShaDesc* __restrict__ descs, uint32_t n,
