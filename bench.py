@@ -733,7 +733,9 @@ def long_leg(args):
                                   f"in {up.sched.nchunks} chunks of {chunk} B per file", "files": F,
                       "file_bytes": S, "nfrag": N, "chunk": chunk},
            "roofline": {"bound": "valu (lane-limited)", "achieved": round(tops, 3), "peak": round(VALU_PEAK_TOPS, 3),
-                        "unit": "Tops/s (int32)", "frac": round(tops / VALU_PEAK_TOPS, 4), "kernel": "sha256_lanes",
+                        "unit": "Tops/s (int32)", "frac": round(tops / VALU_PEAK_TOPS, 4),
+                        "kernel": "sha256_chain2 (pair-lane latency kernel)" if lanes <= 16384 else
+                                  ("sha256_chain" if lanes <= 32768 else "sha256_lanes"),
                         "ms": round(k["sha_ms"], 3), "lanes": lanes, "lane_occupancy": round(lanes / 65536, 4),
                         "note": "one message per lane and SHA-256 is sequential within a message: the fileId "
                                 "chains (4.19M blocks each) bound the run"},
