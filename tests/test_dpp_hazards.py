@@ -1,0 +1,138 @@
+"""Static check of the pair-lane latency kernel's machine code (csrc/sha256.hip,
+sha256_chain2).  gfx9 needs two wait states between a VALU instruction that
+writes a VGPR and a DPP instruction that reads that VGPR through its lane
+permutation (the first source operand); the kernel's DPP adds sit inside asm
+statements the compiler does not look into, so nothing but the instruction
+order keeps that rule.  This test compiles the device code to assembly
+(hipcc cross-compiles without a GPU) and walks every instruction of every
+sha256_chain2 instantiation: for each *_dpp instruction, the register it
+permutes must not have been written by a VALU instruction fewer than two wait
+states earlier (an instruction is one wait state, s_nop N is N + 1)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "distributed-file-storage_amd", "csrc", "sha256.hip")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+def vregs(tok):
+    """Registers named by one operand: v7 -> {7}; v[4:7] -> {4, 5, 6, 7}."""
+    m = re.fullmatch(r"v(\d+)", tok)
+    if m:
+        return {int(m.group(1))}
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return set()
+
+
+def instructions(asm, name):
+    """(mnemonic, operands) of every instruction of the kernels whose symbol
+    contains `name`, in program order."""
+    out, on = [], False
+    for line in asm.splitlines():
+        if re.match(r"^[_A-Za-z0-9]+:", line):
+            on = name in line
+            if on:
+                out.append([])
+            continue
+        if not on:
+            continue
+        t = line.split(";")[0].strip()
+        if not t or t.startswith(".") or t.endswith(":"):
+            continue
+        parts = t.split(None, 1)
+        ops = [o.strip() for o in re.split(r",\s*(?![^\[]*\])", parts[1])] if len(parts) > 1 else []
+        out[-1].append((parts[0], ops))
+        if parts[0] == "s_endpgm":
+            on = False
+    return [k for k in out if k]
+
+
+@pytest.fixture(scope="module")
+def device_asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("no hipcc")
+    out = tmp_path_factory.mktemp("isa") / "sha256.s"
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-Xclang", "-target-feature", "-Xclang",
+           "-packed-fp32-ops", "--cuda-device-only", "-S", "-x", "hip", SRC, "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return out.read_text()
+
+
+def check_dpp_reads(ins):
+    """Number of DPP instructions checked; raises on a DPP source written by a
+    VALU instruction fewer than two wait states earlier."""
+    checked = 0
+    for i, (mn, ops) in enumerate(ins):
+        if "_dpp" not in mn:
+            continue
+        # v_add_u32_dpp vdst, vsrc0 (permuted), vsrc1 <dpp controls>
+        src0 = vregs(ops[1])
+        assert src0, (mn, ops)
+        waits, j = 0, i - 1
+        while j >= 0 and waits < 2:
+            pm, pops = ins[j]
+            if pm.startswith("v_") and pops and vregs(pops[0]) & src0:
+                raise AssertionError(f"{pm} {pops} writes the DPP source of {mn} {ops} {waits} wait states earlier")
+            m = pm == "s_nop" and re.fullmatch(r"(\d+)", pops[0])
+            waits += int(m.group(1)) + 1 if m else 1
+            j -= 1
+        checked += 1
+    return checked
+
+
+def test_pair_lane_kernel_keeps_the_dpp_read_hazard(device_asm):
+    kernels = instructions(device_asm, "sha256_chain2")
+    assert len(kernels) >= 2  # one and two wave pairs per workgroup
+    # 3 DPP adds per round x 64 rounds (+ the block's first) per instantiation
+    assert sum(check_dpp_reads(ins) for ins in kernels) >= 2 * 193
+
+
+GOOD = """
+k_test:
+	v_add3_u32 v5, v5, v6, v4
+	v_add_u32_dpp v3, v3, v5 row_shl:4 row_mask:0xf bank_mask:0x5
+	v_add_u32_dpp v4, v2, v12 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5
+	v_add_u32_dpp v3, v5, v5 row_shr:4 row_mask:0xf bank_mask:0xa
+	s_endpgm
+"""
+
+
+def test_the_checker_sees_a_violation():
+    (ins,) = instructions(GOOD, "k_test")
+    assert check_dpp_reads(ins) == 3
+    # one wait state only between the add3 and the DPP read of its result
+    (bad,) = instructions(GOOD.replace("\tv_add_u32_dpp v4, v2, v12 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n", ""),
+                          "k_test")
+    with pytest.raises(AssertionError):
+        check_dpp_reads(bad)
+    # ... and an s_nop 0 in its place repairs it, a written register range counts too
+    (ok,) = instructions(GOOD.replace("v_add_u32_dpp v4, v2, v12 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5",
+                                      "s_nop 0"), "k_test")
+    assert check_dpp_reads(ok) == 2
+    (rng,) = instructions(GOOD.replace("v_add3_u32 v5, v5, v6, v4", "v_lshlrev_b64 v[2:3], 1, v[8:9]"), "k_test")
+    with pytest.raises(AssertionError):
+        check_dpp_reads(rng)
+
+
+def test_pair_lane_rounds_are_ten_instructions(device_asm):
+    """The point of the kernel: 10 VALU instructions per round in the owner
+    wave's block loop (3 rotates, 3 bit ops, one 3-operand add, 3 DPP adds),
+    with no padding between them."""
+    for ins in instructions(device_asm, "sha256_chain2"):
+        first = next(i for i, (mn, _) in enumerate(ins) if "_dpp" in mn)
+        last = max(i for i, (mn, _) in enumerate(ins) if "_dpp" in mn)
+        body = ins[first:last + 1]
+        n_dpp = sum("_dpp" in mn for mn, _ in body)
+        assert n_dpp == 193
+        valu = sum(mn.startswith("v_") for mn, _ in body)
+        nops = sum(mn == "s_nop" for mn, _ in body)
+        assert valu <= 64 * 10 + 16, valu   # the rounds, plus a few copies the register allocator adds
+        assert nops <= 2, nops
