@@ -1,13 +1,17 @@
-"""Static check of the pair-lane latency kernel's machine code (csrc/sha256.hip,
-sha256_chain2).  gfx9 needs two wait states between a VALU instruction that
-writes a VGPR and a DPP instruction that reads that VGPR through its lane
-permutation (the first source operand); the kernel's DPP adds sit inside asm
-statements the compiler does not look into, so nothing but the instruction
-order keeps that rule.  This test compiles the device code to assembly
-(hipcc cross-compiles without a GPU) and walks every instruction of every
-sha256_chain2 instantiation: for each *_dpp instruction, the register it
-permutes must not have been written by a VALU instruction fewer than two wait
-states earlier (an instruction is one wait state, s_nop N is N + 1)."""
+"""Static checks of the SHA-256 kernels' machine code (csrc/sha256.hip),
+compiled to assembly here (hipcc cross-compiles without a GPU).
+
+1. The pair-lane latency kernel (sha256_chain2).  gfx9 needs two wait states
+   between a VALU instruction that writes a VGPR and a DPP instruction that
+   reads that VGPR through its lane permutation (the first source operand);
+   the kernel's DPP adds sit inside asm statements the compiler does not look
+   into, so nothing but the instruction order keeps that rule.  Every
+   instruction of every sha256_chain2 instantiation is walked: for each *_dpp
+   instruction, the register it permutes must not have been written by a VALU
+   instruction fewer than two wait states earlier (an instruction is one wait
+   state, s_nop N is N + 1).  A round must stay ten instructions.
+2. Every kernel's resources as the compiler reports them: no scratch, and the
+   VGPR counts the persistent kernels' launch geometry assumes."""
 import os
 import re
 import shutil
@@ -54,16 +58,61 @@ def instructions(asm, name):
     return [k for k in out if k]
 
 
-@pytest.fixture(scope="module")
-def device_asm(tmp_path_factory):
-    if not os.path.exists(HIPCC):
-        pytest.skip("no hipcc")
-    out = tmp_path_factory.mktemp("isa") / "sha256.s"
+def compile_device(src, out):
+    """Device code of one source file as assembly; returns (assembly text, the
+    compiler's per-kernel resource remarks)."""
     cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-Xclang", "-target-feature", "-Xclang",
-           "-packed-fp32-ops", "--cuda-device-only", "-S", "-x", "hip", SRC, "-o", str(out)]
+           "-packed-fp32-ops", "--cuda-device-only", "-S", "-Rpass-analysis=kernel-resource-usage", "-x", "hip", src,
+           "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
-    return out.read_text()
+    return out.read_text(), r.stderr
+
+
+@pytest.fixture(scope="module")
+def sha_build(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("no hipcc")
+    return compile_device(SRC, tmp_path_factory.mktemp("isa") / "sha256.s")
+
+
+@pytest.fixture(scope="module")
+def device_asm(sha_build):
+    return sha_build[0]
+
+
+def resources(remarks):
+    """{kernel symbol: {"VGPRs": n, "VGPRs Spill": n, "ScratchSize": n, "Occupancy": n, ...}} from
+    -Rpass-analysis=kernel-resource-usage."""
+    out, cur = {}, None
+    for line in remarks.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([A-Za-z][A-Za-z ]*?)(?: \[[^\]]*\])?: (\d+) \[-Rpass", line)
+        if m and cur is not None:
+            cur[m.group(1)] = int(m.group(2))
+    return out
+
+
+def test_sha_kernels_fit_their_wave_budgets(sha_build):
+    """No kernel of sha256.hip spills to scratch, and the persistent kernels
+    keep the VGPR counts their launch geometry assumes: four waves per SIMD for
+    the hash-only and one-pass instantiations (<= 128 VGPRs), three for the
+    fused-Base64 one (<= 168)."""
+    res = resources(sha_build[1])
+    kernels = {k: v for k, v in res.items() if "sha256_" in k or "static_prep" in k}
+    assert len(kernels) >= 9, sorted(res)
+    for k, v in kernels.items():
+        assert v["ScratchSize"] == 0 and v["VGPRs Spill"] == 0 and v["VGPRs"] > 0, (k, v)
+    def one(sub):
+        (k,) = [k for k in kernels if sub in k]
+        return kernels[k]
+    assert one("12sha256_lanesE")["VGPRs"] <= 128
+    assert one("17sha256_lanes_waitE")["VGPRs"] <= 128
+    assert one("19sha256_b64dec_lanesE")["VGPRs"] <= 128
+    assert one("16sha256_lanes_b64E")["VGPRs"] <= 168
 
 
 def check_dpp_reads(ins):
