@@ -185,3 +185,20 @@ def test_pair_lane_rounds_are_ten_instructions(device_asm):
         nops = sum(mn == "s_nop" for mn, _ in body)
         assert valu <= 64 * 10 + 16, valu   # the rounds, plus a few copies the register allocator adds
         assert nops <= 2, nops
+
+
+@pytest.mark.parametrize("name", ["base64.hip", "gather.hip"])
+def test_stream_kernels_do_not_spill(tmp_path, name):
+    """The HBM-bound kernels: no scratch, no spills; the Base64 encode kernel
+    stays within the 64 VGPRs that let two of its workgroups per CU sit beside
+    three SHA waves per SIMD (3 x 128 + 2 x 64 <= 512)."""
+    if not os.path.exists(HIPCC):
+        pytest.skip("no hipcc")
+    _, remarks = compile_device(os.path.join(os.path.dirname(SRC), name), tmp_path / (name + ".s"))
+    res = resources(remarks)
+    assert res, remarks[-500:]
+    for k, v in res.items():
+        assert v["ScratchSize"] == 0 and v["VGPRs Spill"] == 0, (k, v)
+    if name == "base64.hip":
+        (enc,) = [v for k, v in res.items() if "b64_encode_kernel" in k]
+        assert enc["VGPRs"] <= 64, enc
